@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: Mvoxels/s per RL iteration of the multiview deconvolution path.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): 4-view 512^3 synthetic PSF-blurred bead
+volume, 25^3 PSFs, multiview RL (PSFTYPE INDEPENDENT, lambda 0) -- one *step*
+= one full RL iteration (all views, sequential per-view updates) over the
+volume, inputs resident in HBM.  With N ranks each GPU holds a 512^3 z-slab of
+a 512x512x(512N) volume (weak scaling); the slabs exchange 12-plane halos over
+RCCL before every convolution.  value = all ranks' voxels * steps / max-rank
+time / 1e6.
+
+Also reported: ``roofline`` of the RL pointwise update (quotient + update
+kernels, 28 B per voxel per view) timed with HIP events
+on the session's stream, and ``cpu_baseline`` = the oracle's float32 scipy.fft
+restatement of the same iteration on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--views", type=int, default=4)
+    ap.add_argument("--size", type=int, default=512, help="per-GPU cube edge")
+    ap.add_argument("--ksize", type=int, default=25)
+    ap.add_argument("--psftype", default="INDEPENDENT")
+    ap.add_argument("--lam", type=float, default=0.0)
+    ap.add_argument("--fp16", action="store_true", help="fp16 img/weight storage")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-size", type=int, default=256, help="edge of the CPU-baseline sample")
+    ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline pass")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle (numpy + scipy.fft float32, multithreaded) on a bounded sample:
+    V views of cpu_size^3 with the same PSFs; 1 warm-up + 2 timed iterations."""
+    from oracle import mvdecon_ref as ref
+    from spim_registration_amd import synthetic
+
+    n = args.cpu_size
+    cores = min(os.cpu_count() or 1, 16)
+    imgs, ws, psfs, _ = synthetic.make_views((n, n, n), args.views, config_id=1,
+                                             ksize=(args.ksize,) * 3, weights="blend")
+    k1s, k2s = ref.prepare_kernels(psfs, ref.PSFTYPE[args.psftype], 8)
+    _, avg = ref.first_iteration(imgs)
+    psi = np.full(imgs[0].shape, np.float32(avg), np.float32)
+    psi, _ = ref.run_iteration(psi, imgs, ws, k1s, k2s, args.lam, "f32", cores)
+    t0 = time.perf_counter()
+    iters = 2
+    for _ in range(iters):
+        psi, _ = ref.run_iteration(psi, imgs, ws, k1s, k2s, args.lam, "f32", cores)
+    dt = (time.perf_counter() - t0) / iters
+    return {"value": round(n ** 3 / dt / 1e6, 3), "unit": "Mvoxels/s per RL iteration",
+            "cores": cores, "kind": "port",
+            "sample": f"{args.views}-view {n}^3, {args.ksize}^3 PSF, {args.psftype}, 2 timed iterations "
+                      f"(numpy + scipy.fft float32, workers={cores}); stand-in for the Java/ImgLib2 CPU path"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from spim_registration_amd import synthetic
+    from spim_registration_amd.decon import PSFTYPE, Session
+    from spim_registration_amd.distributed import broadcast_comm_id, env_rank
+
+    rank, world, local = env_rank()
+    if world != args.gpus and "RANK" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+    comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
+
+    n = args.size
+    V = args.views
+    nz_g = n * world
+    imgs, ws, psfs = synthetic.make_views_torch((n, n, n), V, config_id=1 + rank,
+                                                ksize=(args.ksize,) * 3, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+    sess = Session((n, n, n), device=local, nranks=world, rank=rank, comm_id=comm_id,
+                   nz_global=nz_g, z_offset=rank * n, storage_fp16=args.fp16)
+    for i, w, k in zip(imgs, ws, psfs):
+        sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
+    del imgs, ws
+    torch.cuda.empty_cache()
+    sess.init(PSFTYPE[args.psftype])
+    sess.init_psi()
+    M = sess.fft_dims(0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # warm-up (rocFFT kernels, caches)
+    if args.warmup:
+        sess.run(args.warmup, args.lam)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(args.steps, args.lam)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    barrier()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    ms_per_step = dt / max(args.steps, 1) * 1e3
+    n_vox_total = n * n * nz_g
+    value = n_vox_total * args.steps / dt / 1e6
+
+    # roofline pass: HIP events on the session stream around every kernel class
+    roofline = None
+    kernel_ms = None
+    it_roof = None
+    if not args.no_timing:
+        sess.enable_timing(True)
+        sess.run(2, args.lam)
+        tm = sess.timing()
+        sess.enable_timing(False)
+        names = ["update_pad", "quotient_pad", "r2c", "spec_mul", "c2r", "halo_exchange", "stats_reduce"]
+        kernel_ms = {nm: {"total_ms": round(tm[i], 4), "launches": int(tm[8 + i]),
+                          "avg_ms": round(tm[i] / tm[8 + i], 5) if tm[8 + i] else None}
+                     for i, nm in enumerate(names)}
+        N = n ** 3
+        t_upd = tm[0] / max(tm[8], 1)       # includes the one initial pad launch per run
+        t_quo = tm[1] / max(tm[9], 1)
+        bytes_pw = 28.0 * N                 # 12 B quotient + 16 B update per voxel per view (8d)
+        achieved = bytes_pw / ((t_upd + t_quo) * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "k_quotient_pad + k_update_pad (RL pointwise update, per view)",
+                    "algorithmic_bytes_per_view": int(bytes_pw)}
+        Mlog = M[0] * M[1] * M[2]
+        b_iter = V * (28.0 * N + 56.0 * Mlog)
+        t_iter = ms_per_step * 1e-3
+        it_roof = {"achieved": round(b_iter / t_iter / 1e9, 1), "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": round(b_iter / t_iter / 1e9 / HBM_PEAK_GBS, 4),
+                   "model": "V*(28N + 56M) bytes per iteration (SURVEY 8d)", "M": list(M)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": "Mvoxels/sec per RL iter, multiview deconv",
+            "value": round(value, 2),
+            "unit": "Mvoxels/s per RL iteration",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" + ("(fp16 img/w storage)" if args.fp16 else ""),
+            "data": "synthetic (seeded bead stacks generated on the GPU, SURVEY 8d)",
+            "config": {"workload": f"{V}-view {n}^3 per GPU (global {n}x{n}x{nz_g}), "
+                                   f"{args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}",
+                       "views": V, "volume_xyz": [n, n, nz_g], "psf": [args.ksize] * 3,
+                       "fft_dims_xyz": list(M), "parallelism": f"z-slab x{world} (RCCL halo)"},
+            "roofline": roofline,
+            "roofline_iteration": it_roof,
+            "kernel_ms": kernel_ms,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

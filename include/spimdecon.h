@@ -1,0 +1,239 @@
+/*
+ * spimdecon.h -- C-ABI of libspimdecon.so, the MI355X-native drop-in for the
+ * multiview Richardson-Lucy deconvolution + DoG bead-detection hot path of
+ * PreibischLab/SPIM_Registration.
+ *
+ * Reference interfaces replaced (paths under /root/reference/src/main/java/):
+ *   - spim/process/cuda/CUDAFourierConvolution.java:4-10      (FourierConvolutionCUDALib, JNA)
+ *   - spim/process/cuda/CUDAStandardFunctions.java:15-23      (device query, JNA)
+ *   - spim/process/cuda/CUDASeparableConvolution.java:13-21   (SeparableConvolutionCUDALib, JNA)
+ *   - spim/process/fusion/deconvolution/MVDeconvolution.java:73-444 (RL loop; new session API)
+ *   - spim/process/fusion/deconvolution/MVDeconFFT.java:162-303     (kernel preparation)
+ *   - spim/process/interestpointdetection/ProcessDOG.java:40-178    (DoG pass)
+ *
+ * Conventions
+ *   - Plain C types only; every pointer is caller-owned and only read/written
+ *     during the call.  Volumes are x-fastest float32 (ImgLib2 ArrayImg order).
+ *   - JNA type mapping: Java boolean -> int32_t, Java long -> int64_t,
+ *     float[]/int[] -> pointers (JNA copies arrays in and back out).
+ *   - Status codes: 0 = OK, negative = error; the message of the last error of
+ *     the calling thread is returned by spimdecon_last_error().
+ *   - No CPU fallback: a negative/invalid device id or a missing GPU is an
+ *     error (status SPIMDECON_ERR_DEVICE), never a silent CPU path.
+ */
+#ifndef SPIMDECON_H
+#define SPIMDECON_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPIMDECON_OK               0
+#define SPIMDECON_ERR_ARG         -1
+#define SPIMDECON_ERR_DEVICE      -2
+#define SPIMDECON_ERR_HIP         -3
+#define SPIMDECON_ERR_FFT         -4
+#define SPIMDECON_ERR_COMM        -5
+#define SPIMDECON_ERR_STATE       -6
+#define SPIMDECON_ERR_OOM         -7
+
+/* last error message of the calling thread ("" if none) */
+const char* spimdecon_last_error(void);
+/* library version string, e.g. "spimdecon 0.1.0 gfx950 rocfft 1.0.36" */
+const char* spimdecon_version(void);
+
+/* ======================================================================
+ * 1. Legacy FourierConvolutionCUDALib ABI
+ *    spim/process/cuda/CUDAFourierConvolution.java:9-10; called from
+ *    spim/process/fusion/deconvolution/MVDeconFFTThreads.java:65-68,88-91.
+ * ====================================================================== */
+
+/* In-place circular 3D convolution of one block with a kernel whose centre
+ * kernelDim/2 is moved to the origin (the block already carries the K-1 halo).
+ * imDim / kernelDim are REVERSED: {nz, ny, nx} (MVDeconFFTThreads.java:136-144).
+ * Thread-safe: one Java thread per device calls this concurrently
+ * (MVDeconFFT.java:424-446); per-device plan and stream caches.
+ * Java declares `void`; the int status is ignored by such a binding. */
+int convolution3DfftCUDAInPlace(float* im, const int* imDim,
+                                const float* kernel, const int* kernelDim,
+                                int devCUDA);
+
+/* Out-of-place variant (declared at CUDAFourierConvolution.java:9, never
+ * called by the reference).  Returns a buffer owned by the library that must
+ * be released with spimdecon_free(); NULL on error. */
+float* convolution3DfftCUDA(const float* im, const int* imDim,
+                            const float* kernel, const int* kernelDim,
+                            int devCUDA);
+void spimdecon_free(void* p);
+
+/* ======================================================================
+ * 2. Device query ABI -- spim/process/cuda/CUDAStandardFunctions.java:15-23,
+ *    consumer spim/process/cuda/CUDATools.java:35-192.
+ * ====================================================================== */
+int     getNumDevicesCUDA(void);                       /* -1 = driver error, 0 = none */
+void    getNameDeviceCUDA(int devCUDA, char* name);    /* name: >= 256 bytes */
+int64_t getMemDeviceCUDA(int devCUDA);
+int64_t getFreeMemDeviceCUDA(int devCUDA);
+/* gfx950 is reported as "compute capability" 9.5 (major 9, minor 5) */
+int     getCUDAcomputeCapabilityMajorVersion(int devCUDA);
+int     getCUDAcomputeCapabilityMinorVersion(int devCUDA);
+
+/* ======================================================================
+ * 3. SeparableConvolutionCUDALib ABI -- spim/process/cuda/CUDASeparableConvolution.java:13-17;
+ *    caller spim/process/cuda/CUDASeparableConvolutionFunctions.java:176-196.
+ *    In-place separable convolution of a w*h*d x-fastest image with centred
+ *    kernels of length N (7/15/31/63/127).  Dims NOT reversed.
+ *    outofbounds: 0 = zero, 1 = value (outofboundsvalue), 2 = extend border
+ *    pixel; 3 = mirror-single (extension used by this library's DoG pass).
+ *    Returns 1 (Java true) on success, 0 on failure.
+ * ====================================================================== */
+int32_t convolve_7  (float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                     int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
+                     int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
+int32_t convolve_15 (float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                     int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
+                     int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
+int32_t convolve_31 (float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                     int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
+                     int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
+int32_t convolve_63 (float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                     int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
+                     int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
+int32_t convolve_127(float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                     int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
+                     int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
+
+/* ======================================================================
+ * 4. Kernel preparation -- spim/process/fusion/deconvolution/MVDeconFFT.java:162-303
+ *    (MVDeconInput.init order, AdjustInput.normImg quirk with ij_threads).
+ * ====================================================================== */
+#define MVD_PSF_OPTIMIZATION_II     0   /* MVDeconFFT.PSFTYPE ordinals, MVDeconFFT.java:28 */
+#define MVD_PSF_OPTIMIZATION_I      1
+#define MVD_PSF_EFFICIENT_BAYESIAN  2
+#define MVD_PSF_INDEPENDENT         3
+
+/* kdims: 3*nviews ints, per view {kx, ky, kz} (odd).  k1_out[v] receives the
+ * normalised kernel1, k2_out[v] kernel2 (both kx*ky*kz floats).  Runs on GPU
+ * devCUDA. */
+int mvd_prepare_kernels(int nviews, const float* const* k1_in, const int* kdims,
+                        int psftype, int ij_threads,
+                        float* const* k1_out, float* const* k2_out, int devCUDA);
+
+/* ======================================================================
+ * 5. GPU-resident RL session (replaces MVDeconvolution.runIteration's
+ *    per-view convolve1 -> quotient -> convolve2 -> update loop,
+ *    MVDeconvolution.java:333-444, and the init/mask of :95-187).
+ * ====================================================================== */
+typedef struct mvd_session mvd_session;
+
+typedef struct mvd_params {
+    int64_t dims[3];        /* {nx, ny, nz} of THIS rank's z-range of psi          */
+    int64_t nz_global;      /* global nz (== dims[2] for a single rank)            */
+    int64_t z_offset;       /* first global z plane owned by this rank             */
+    int     device;         /* HIP device id (>= 0)                                */
+    int     local_slabs;    /* z-slabs held by this process (>= 1); >1 = virtual shards */
+    int     nranks;         /* processes in the RCCL communicator (1 = none)       */
+    int     rank;
+    const char* comm_id;    /* 128-byte RCCL unique id (NULL when nranks == 1)     */
+    int     storage_fp16;   /* 1: img/weights stored as fp16 (config-5 mode)       */
+    int     fft_pad_policy; /* 0 = smallest 2^a3^b5^c7^d >= n+K-1 (default)        */
+    int     halo[3];        /* max kernel half size {cx,cy,cz}; 0 = derive from views */
+    int     ij_threads;     /* pinned reference thread count for the normImg quirk  */
+    int     reserved[8];
+} mvd_params;
+
+/* fills *p with defaults (local_slabs=1, nranks=1, ij_threads=8, ...) */
+void mvd_params_default(mvd_params* p);
+
+/* 128-byte RCCL unique id for rank 0 to broadcast (torch.distributed / MPI) */
+int mvd_comm_unique_id(char* out128);
+
+/* global [z0, z1) of part `idx` of `nparts` over nz planes (balanced split) */
+int mvd_slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1);
+
+int  mvd_create(const mvd_params* params, mvd_session** out);
+void mvd_destroy(mvd_session* h);
+
+/* Adds one view (MVDeconInput.add order).  img/weight: this rank's z-range,
+ * dims = params.dims; kernel1: raw (un-normalised) PSF of kdims {kx,ky,kz}.
+ * Views are only staged here; mvd_init() builds kernels and uploads. */
+int mvd_add_view(mvd_session* h, const float* img, const float* weight,
+                 const float* kernel1, const int* kdims);
+/* Same, but img/weight are device pointers on params.device (copied). */
+int mvd_add_view_device(mvd_session* h, const float* d_img, const float* d_weight,
+                        const float* kernel1, const int* kdims);
+
+/* MVDeconInput.init(type): normalises kernel1 and builds kernel2 for all
+ * views (MVDeconFFT.java:162-303) then computes the kernel spectra. */
+int mvd_init(mvd_session* h, int psftype);
+/* Alternative to mvd_init: kernels already prepared by the caller
+ * (MVDeconFFT.getKernel1/2, MVDeconFFT.java:352-353). */
+int mvd_set_kernels(mvd_session* h, int view, const float* k1, const float* k2);
+/* read back prepared kernels (kx*ky*kz floats each) */
+int mvd_get_kernels(mvd_session* h, int view, float* k1, float* k2);
+
+/* psi initialisation (MVDeconvolution.java:95-127).  psi == NULL: first-iteration
+ * average fusion (FirstIteration.java, NaN -> 0.5); else the given image with
+ * the checkNumbers clamp (<= 0 -> minValue). *avg_out may be NULL. */
+int mvd_init_psi(mvd_session* h, const float* psi_or_null, double* avg_out);
+
+/* runs `iters` RL iterations (sequential per-view updates).  lambda > 0:
+ * Tikhonov.  stats (may be NULL): iters*nviews*2 doubles {sumChange, maxChange}
+ * reduced over all slabs and ranks. */
+int mvd_run(mvd_session* h, int iters, double lambda, double* stats);
+
+/* final mask: psi = 0 where no view has data (MVDeconvolution.java:180-187) */
+int mvd_apply_mask(mvd_session* h);
+
+/* copy this rank's psi to host (dims of params) */
+int mvd_get_psi(mvd_session* h, float* out);
+/* device pointer of local slab s's psi (valid until mvd_destroy) */
+float* mvd_psi_device(mvd_session* h, int slab);
+
+/* padded FFT dims {Mx, My, Mz} of local slab s (info/bench) */
+int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3);
+/* HIP stream the session launches on (hipStream_t as void*) */
+void* mvd_stream(mvd_session* h);
+/* per-kernel timing: when enabled, mvd_run records HIP events around every
+ * kernel class; mvd_timing returns the accumulated ms per class:
+ * [0] pad/update, [1] quotient, [2] r2c, [3] spectral multiply, [4] c2r,
+ * [5] halo exchange, [6] launches counted for [0] (update kernel count) ... */
+int mvd_enable_timing(mvd_session* h, int on);
+int mvd_timing(mvd_session* h, double* out16);
+
+/* ======================================================================
+ * 6. DoG bead detection -- spim/process/interestpointdetection/ProcessDOG.java:40-178
+ * ====================================================================== */
+typedef struct spim_dog_params {
+    float   sigma;           /* default 1.8 (DifferenceOfGaussian.java:36)          */
+    float   threshold;       /* default 0.008 (DifferenceOfGaussian.java:37)        */
+    int     localization;    /* 0 = none (threshold), 1 = quadratic (threshold/10)  */
+    double  image_sigma[3];  /* default 0.5 each; min(imageSigma, sigma) applied    */
+    int32_t find_min;
+    int32_t find_max;
+    double  min_intensity;   /* NaN -> image min/max                                */
+    double  max_intensity;
+    int     ij_threads;      /* peak ordering: lists by x % T (InteractiveIntegral.java:394) */
+    int     device;
+} spim_dog_params;
+
+typedef struct spim_peak {
+    int32_t x, y, z;
+    float   intensity;       /* |dog| */
+    int32_t is_min, is_max;
+} spim_peak;
+
+void spim_dog_params_default(spim_dog_params* p);
+
+/* img: dims {nx, ny, nz} x-fastest (not modified).  dog_out (optional, may be
+ * NULL) receives the DoG image.  peaks: capacity max_peaks, *npeaks = total
+ * found (may exceed max_peaks: then only max_peaks were written). */
+int spim_dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p,
+                     float* dog_out, spim_peak* peaks, int64_t max_peaks, int64_t* npeaks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPIMDECON_H */

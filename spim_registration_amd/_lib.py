@@ -1,0 +1,154 @@
+"""ctypes binding of libspimdecon.so (C-ABI declared in include/spimdecon.h).
+
+The binding mirrors what the reference's JNA interfaces would bind
+(``spim/process/cuda/CUDAFourierConvolution.java``, ``CUDAStandardFunctions.java``,
+``CUDASeparableConvolution.java``): Java ``boolean`` -> ``int32``, ``long`` ->
+``int64``, arrays -> pointers.  Loading never falls back to anything: if the
+in-tree library is missing the import of the compute API fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libspimdecon.so"
+
+_i32, _i64, _f32, _f64 = C.c_int32, C.c_int64, C.c_float, C.c_double
+_pf = C.POINTER(C.c_float)
+_pi = C.POINTER(C.c_int)
+_pi64 = C.POINTER(C.c_int64)
+_pd = C.POINTER(C.c_double)
+
+
+class MvdParams(C.Structure):
+    _fields_ = [
+        ("dims", C.c_int64 * 3),
+        ("nz_global", C.c_int64),
+        ("z_offset", C.c_int64),
+        ("device", C.c_int),
+        ("local_slabs", C.c_int),
+        ("nranks", C.c_int),
+        ("rank", C.c_int),
+        ("comm_id", C.c_char_p),
+        ("storage_fp16", C.c_int),
+        ("fft_pad_policy", C.c_int),
+        ("halo", C.c_int * 3),
+        ("ij_threads", C.c_int),
+        ("reserved", C.c_int * 8),
+    ]
+
+
+class DogParams(C.Structure):
+    _fields_ = [
+        ("sigma", C.c_float),
+        ("threshold", C.c_float),
+        ("localization", C.c_int),
+        ("image_sigma", C.c_double * 3),
+        ("find_min", C.c_int32),
+        ("find_max", C.c_int32),
+        ("min_intensity", C.c_double),
+        ("max_intensity", C.c_double),
+        ("ij_threads", C.c_int),
+        ("device", C.c_int),
+    ]
+
+
+class Peak(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("z", C.c_int32),
+                ("intensity", C.c_float), ("is_min", C.c_int32), ("is_max", C.c_int32)]
+
+
+# name -> (restype, argtypes); exactly the declarations of include/spimdecon.h
+SIGNATURES = {
+    "spimdecon_last_error": (C.c_char_p, []),
+    "spimdecon_version": (C.c_char_p, []),
+    "convolution3DfftCUDAInPlace": (C.c_int, [_pf, _pi, _pf, _pi, C.c_int]),
+    "convolution3DfftCUDA": (_pf, [_pf, _pi, _pf, _pi, C.c_int]),
+    "spimdecon_free": (None, [C.c_void_p]),
+    "getNumDevicesCUDA": (C.c_int, []),
+    "getNameDeviceCUDA": (None, [C.c_int, C.c_char_p]),
+    "getMemDeviceCUDA": (_i64, [C.c_int]),
+    "getFreeMemDeviceCUDA": (_i64, [C.c_int]),
+    "getCUDAcomputeCapabilityMajorVersion": (C.c_int, [C.c_int]),
+    "getCUDAcomputeCapabilityMinorVersion": (C.c_int, [C.c_int]),
+    "mvd_prepare_kernels": (C.c_int, [C.c_int, C.POINTER(_pf), _pi, C.c_int, C.c_int,
+                                      C.POINTER(_pf), C.POINTER(_pf), C.c_int]),
+    "mvd_params_default": (None, [C.POINTER(MvdParams)]),
+    "mvd_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "mvd_slab_range": (C.c_int, [_i64, C.c_int, C.c_int, _pi64, _pi64]),
+    "mvd_create": (C.c_int, [C.POINTER(MvdParams), C.POINTER(C.c_void_p)]),
+    "mvd_destroy": (None, [C.c_void_p]),
+    "mvd_add_view": (C.c_int, [C.c_void_p, _pf, _pf, _pf, _pi]),
+    "mvd_add_view_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, _pf, _pi]),
+    "mvd_init": (C.c_int, [C.c_void_p, C.c_int]),
+    "mvd_set_kernels": (C.c_int, [C.c_void_p, C.c_int, _pf, _pf]),
+    "mvd_get_kernels": (C.c_int, [C.c_void_p, C.c_int, _pf, _pf]),
+    "mvd_init_psi": (C.c_int, [C.c_void_p, _pf, _pd]),
+    "mvd_run": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _pd]),
+    "mvd_apply_mask": (C.c_int, [C.c_void_p]),
+    "mvd_get_psi": (C.c_int, [C.c_void_p, _pf]),
+    "mvd_psi_device": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "mvd_fft_dims": (C.c_int, [C.c_void_p, C.c_int, _pi64]),
+    "mvd_stream": (C.c_void_p, [C.c_void_p]),
+    "mvd_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "mvd_timing": (C.c_int, [C.c_void_p, _pd]),
+    "convolve_7": (_i32, [_pf, _pf, _pf, _pf, C.c_int, C.c_int, C.c_int, _i32, _i32, _i32,
+                          C.c_int, C.c_float, C.c_int]),
+    "spim_dog_params_default": (None, [C.POINTER(DogParams)]),
+    "spim_dog_compute": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf, C.POINTER(Peak),
+                                   _i64, _pi64]),
+}
+for _n in (15, 31, 63, 127):
+    SIGNATURES[f"convolve_{_n}"] = SIGNATURES["convolve_7"]
+
+_lib = None
+
+
+class SpimDeconError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"libspimdecon status {status}: {msg}")
+        self.status = status
+
+
+def load():
+    """Loads the in-tree library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"{LIB_PATH} not found: build it with `python -m spim_registration_amd.build` "
+            "(there is no CPU fallback)")
+    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().spimdecon_last_error().decode(errors="replace")
+
+
+def check(status: int):
+    if status != 0:
+        raise SpimDeconError(status, last_error())
+
+
+def fptr(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous, (a.dtype, a.flags)
+    return a.ctypes.data_as(_pf)
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_pi)
+
+
+def num_devices() -> int:
+    return int(load().getNumDevicesCUDA())

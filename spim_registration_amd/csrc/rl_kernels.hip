@@ -1,0 +1,451 @@
+// rl_kernels.hip -- HBM-bound pointwise / halo-pad kernels of the RL iteration.
+//
+// Padded volume layout (fft.hpp): circular placement -- padded coordinate q
+// maps to image coordinate s(q) = q < n + c ? q : q - M, so the image interior
+// sits at q = s (row-aligned with the unpadded arrays) and the halo of width c
+// wraps around the end of each axis.  Every kernel walks the padded volume
+// one wave per padded row (wave-uniform z/y decode, lanes over x).
+//
+// Float semantics follow the Java reference exactly (no contraction):
+//   quotient  img > 0 ? img / blurred : 1             MVDeconvolution.java:473-525
+//   update    computeNextValue + Tikhonov (f64 sqrt)   MVDeconvolution.java:671-705
+#include "rl_kernels.hpp"
+
+namespace spimdecon {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ int64_t s_of_q(int64_t q, int64_t n, int c, int64_t M) {
+    return q < n + c ? q : q - M;
+}
+
+// extendMirrorSingle index (numpy 'reflect'), periodic for far coordinates
+__device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
+    if (n == 1) return 0;
+    const int64_t p = 2 * (n - 1);
+    int64_t j = s % p;
+    if (j < 0) j += p;
+    return j >= n ? p - j : j;
+}
+
+template <int S>
+__device__ __forceinline__ float ld(const void* p, int64_t i) {
+    if constexpr (S == 0) {
+        return static_cast<const float*>(p)[i];
+    } else {
+        return __half2float(static_cast<const __half*>(p)[i]);
+    }
+}
+
+// MVDeconvolution.computeNextValue (:671-703), float op order kept.
+__device__ __forceinline__ float next_value(float last, float integral, float weight, double lambda) {
+    const float value = __fmul_rn(last, integral);
+    float adjusted;
+    if (value > 0.0f) {
+        if (lambda > 0.0)
+            adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
+        else
+            adjusted = value;
+    } else {
+        adjusted = kMinValue;
+    }
+    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
+    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
+}
+
+struct RowMap {
+    bool skip;       // internal z halo (filled by the exchange) or out-of-range row
+    bool zout;       // outside the global volume in z
+    bool yout;
+    int64_t lz, ly;  // mirror-mapped local source row
+    bool zin, yin;   // row is an interior row (s == mirror(s))
+    int64_t sy;
+};
+
+__device__ __forceinline__ RowMap map_row(const SlabGeom& g, int64_t row) {
+    RowMap r;
+    const int64_t qz = row / g.My;
+    const int64_t qy = row - qz * g.My;
+    const int64_t sz = s_of_q(qz, g.nz, g.cz, g.Mz);
+    const int64_t gz = g.z0 + sz;
+    const bool global_in = gz >= 0 && gz < g.nzg;
+    r.skip = global_in && (sz < 0 || sz >= g.nz);
+    r.zout = !global_in;
+    r.lz = mirror_idx(gz, g.nzg) - g.z0;
+    r.zin = (sz >= 0 && sz < g.nz);
+    if (!r.skip && (r.lz < 0 || r.lz >= g.nz)) r.skip = true;  // host guarantees this never happens
+    r.sy = s_of_q(qy, g.ny, g.cy, g.My);
+    r.yout = r.sy < 0 || r.sy >= g.ny;
+    r.ly = mirror_idx(r.sy, g.ny);
+    r.yin = !r.yout;
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pad_mirror(SlabGeom g, const float* __restrict__ psi,
+                                                        float* __restrict__ Ra) {
+    const int lane = threadIdx.x & 63;
+    const int64_t rows = g.My * g.Mz;
+    for (int64_t row = int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6); row < rows;
+         row += int64_t(gridDim.x) * kWaves) {
+        const RowMap r = map_row(g, row);
+        if (r.skip) continue;
+        const float* src = psi + (r.lz * g.ny + r.ly) * g.nx;
+        float* dst = Ra + row * g.Sx;
+        for (int64_t qx = lane; qx < g.Mx; qx += 64) {
+            const int64_t lx = mirror_idx(s_of_q(qx, g.nx, g.cx, g.Mx), g.nx);
+            dst[qx] = src[lx];
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_quotient_pad(SlabGeom g, const void* __restrict__ img,
+                                                          const float* __restrict__ Ra,
+                                                          float* __restrict__ Rb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t rows = g.My * g.Mz;
+    for (int64_t row = int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6); row < rows;
+         row += int64_t(gridDim.x) * kWaves) {
+        const RowMap r = map_row(g, row);
+        if (r.skip) continue;
+        float* dst = Rb + row * g.Sx;
+        if (r.zout || r.yout) {
+            for (int64_t qx = lane; qx < g.Mx; qx += 64) dst[qx] = 1.0f;
+            continue;
+        }
+        // interior row: q == s, Ra row == this row
+        const float* blurred = Ra + row * g.Sx;
+        const int64_t base = (r.lz * g.ny + r.ly) * g.nx;
+        for (int64_t qx = lane; qx < g.Mx; qx += 64) {
+            float out = 1.0f;
+            if (qx < g.nx) {
+                const float iv = ld<S>(img, base + qx);
+                if (iv > 0.0f) out = __fdiv_rn(iv, blurred[qx]);
+            }
+            dst[qx] = out;
+        }
+    }
+}
+
+__device__ __forceinline__ void block_reduce_sum_max(double& sum, float& mx, double* sh_sum,
+                                                     float* sh_max) {
+    for (int off = 32; off > 0; off >>= 1) {
+        sum += __shfl_xor(sum, off, 64);
+        mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sh_sum[wid] = sum;
+        sh_max[wid] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWaves; ++w) {
+            sum += sh_sum[w];
+            mx = fmaxf(mx, sh_max[w]);
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_update_pad(SlabGeom g, const float* __restrict__ psi_in,
+                                                        const float* __restrict__ Rb,
+                                                        const void* __restrict__ w, double lambda,
+                                                        float* __restrict__ psi_out,
+                                                        float* __restrict__ Ra,
+                                                        double* __restrict__ partials,
+                                                        int write_pad) {
+    __shared__ double sh_sum[kWaves];
+    __shared__ float sh_max[kWaves];
+    const int lane = threadIdx.x & 63;
+    const int64_t rows = g.My * g.Mz;
+    double sum = 0.0;
+    float mx = -1.0f;
+    for (int64_t row = int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6); row < rows;
+         row += int64_t(gridDim.x) * kWaves) {
+        const RowMap r = map_row(g, row);
+        if (r.skip) continue;
+        const bool interior_row = r.zin && r.yin;
+        if (!write_pad && !interior_row) continue;
+        const int64_t vbase = (r.lz * g.ny + r.ly) * g.nx;
+        const float* integ = Rb + (r.lz * g.My + r.ly) * g.Sx;  // interior slot of the source row
+        float* dst = Ra + row * g.Sx;
+        for (int64_t qx = lane; qx < g.Mx; qx += 64) {
+            const int64_t sx = s_of_q(qx, g.nx, g.cx, g.Mx);
+            const bool xin = sx >= 0 && sx < g.nx;
+            if (!write_pad && !xin) continue;
+            const int64_t lx = mirror_idx(sx, g.nx);
+            const float last = psi_in[vbase + lx];
+            const float nv = next_value(last, integ[lx], ld<S>(w, vbase + lx), lambda);
+            if (write_pad) dst[qx] = nv;
+            if (interior_row && xin) {
+                psi_out[vbase + lx] = nv;
+                const float ch = fabsf(__fsub_rn(nv, last));
+                sum += (double)ch;
+                mx = fmaxf(mx, ch);
+            }
+        }
+    }
+    block_reduce_sum_max(sum, mx, sh_sum, sh_max);
+    if (threadIdx.x == 0) {
+        partials[2 * blockIdx.x] = sum;
+        partials[2 * blockIdx.x + 1] = (double)mx;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce_partials(const double* __restrict__ partials,
+                                                             int64_t n, double* out, int accumulate) {
+    __shared__ double sh_sum[kWaves];
+    __shared__ float sh_max_unused[kWaves];
+    __shared__ double sh_max[kWaves];
+    double sum = 0.0, mx = -1.0;
+    for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+        sum += partials[2 * i];
+        mx = fmax(mx, partials[2 * i + 1]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sum += __shfl_xor(sum, off, 64);
+        mx = fmax(mx, __shfl_xor(mx, off, 64));
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sh_sum[wid] = sum;
+        sh_max[wid] = mx;
+    }
+    (void)sh_max_unused;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w2 = 1; w2 < kWaves; ++w2) {
+            sum += sh_sum[w2];
+            mx = fmax(mx, sh_max[w2]);
+        }
+        if (accumulate) {
+            out[0] += sum;
+            out[1] = fmax(out[1], mx);
+        } else {
+            out[0] = sum;
+            out[1] = mx;
+        }
+    }
+}
+
+// ComplexFloatType.mul: (a*c - b*d, a*d + b*c)
+__global__ __launch_bounds__(kBlock) void k_spec_mul(float4* __restrict__ C,
+                                                      const float4* __restrict__ K, int64_t n2,
+                                                      float2* __restrict__ Ct,
+                                                      const float2* __restrict__ Kt, int tail) {
+    const int64_t stride = int64_t(gridDim.x) * kBlock;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n2; i += stride) {
+        const float4 a = C[i];
+        const float4 k = K[i];
+        float4 r;
+        r.x = a.x * k.x - a.y * k.y;
+        r.y = a.x * k.y + a.y * k.x;
+        r.z = a.z * k.z - a.w * k.w;
+        r.w = a.z * k.w + a.w * k.z;
+        C[i] = r;
+    }
+    if (tail && blockIdx.x == 0 && threadIdx.x == 0) {
+        const float2 a = *Ct;
+        const float2 k = *Kt;
+        *Ct = make_float2(a.x * k.x - a.y * k.y, a.x * k.y + a.y * k.x);
+    }
+}
+
+__global__ void k_place_kernel(SlabGeom g, const float* __restrict__ k, int kx, int ky, int kz,
+                               float scale, float* __restrict__ R) {
+    const int64_t n = int64_t(kx) * ky * kz;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t jx = i % kx;
+        const int64_t jy = (i / kx) % ky;
+        const int64_t jz = i / (int64_t(kx) * ky);
+        int64_t qx = (jx - kx / 2) % g.Mx; if (qx < 0) qx += g.Mx;
+        int64_t qy = (jy - ky / 2) % g.My; if (qy < 0) qy += g.My;
+        int64_t qz = (jz - kz / 2) % g.Mz; if (qz < 0) qz += g.Mz;
+        // kernels larger than the FFT volume wrap (accumulate): atomic keeps it exact for overlaps
+        atomicAdd(&R[(qz * g.My + qy) * g.Sx + qx], k[i] * scale);
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void k_first_iteration(int64_t n, int nviews,
+                                                             const void* const* __restrict__ imgs,
+                                                             double* __restrict__ partials) {
+    __shared__ double sh_a[kWaves];
+    __shared__ double sh_b[kWaves];
+    double msum = 0.0, cnt = 0.0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * kBlock) {
+        double s = 0.0;
+        int c = 0;
+        for (int v = 0; v < nviews; ++v) {
+            const double x = (double)ld<S>(imgs[v], i);
+            if (x > 0.0) {
+                s += x;
+                ++c;
+            }
+        }
+        if (c > 0) {
+            msum += s / (double)c;
+            cnt += 1.0;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        msum += __shfl_xor(msum, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sh_a[wid] = msum;
+        sh_b[wid] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWaves; ++w) {
+            msum += sh_a[w];
+            cnt += sh_b[w];
+        }
+        partials[2 * blockIdx.x] = msum;
+        partials[2 * blockIdx.x + 1] = cnt;
+    }
+}
+
+__global__ void k_fill(float* p, int64_t n, float v) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x)
+        p[i] = v;
+}
+
+__global__ void k_clamp_min(float* p, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x)
+        if (p[i] <= 0.0f) p[i] = kMinValue;
+}
+
+template <int S>
+__global__ void k_mask(float* psi, int64_t n, int nviews, const void* const* __restrict__ imgs) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x) {
+        bool any = false;
+        for (int v = 0; v < nviews; ++v) any |= ld<S>(imgs[v], i) > 0.0f;
+        if (!any) psi[i] = 0.0f;
+    }
+}
+
+__global__ void k_to_half(const float* __restrict__ in, __half* __restrict__ out, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += int64_t(gridDim.x) * blockDim.x)
+        out[i] = __float2half(in[i]);
+}
+
+inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap = 256 * 16) {
+    int64_t b = ceil_div(work, per_block);
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return unsigned(b);
+}
+
+}  // namespace
+
+void launch_pad_mirror(const SlabGeom& g, const float* psi, float* Ra, hipStream_t s) {
+    const unsigned grid = grid_for(g.My * g.Mz, kWaves);
+    hipLaunchKernelGGL(k_pad_mirror, dim3(grid), dim3(kBlock), 0, s, g, psi, Ra);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_quotient_pad(const SlabGeom& g, Store st, const void* img, const float* Ra, float* Rb,
+                         hipStream_t s) {
+    const unsigned grid = grid_for(g.My * g.Mz, kWaves);
+    if (st == Store::F32)
+        hipLaunchKernelGGL(k_quotient_pad<0>, dim3(grid), dim3(kBlock), 0, s, g, img, Ra, Rb);
+    else
+        hipLaunchKernelGGL(k_quotient_pad<1>, dim3(grid), dim3(kBlock), 0, s, g, img, Ra, Rb);
+    SD_HIP(hipGetLastError());
+}
+
+int64_t launch_update_pad(const SlabGeom& g, Store st, const float* psi_in, const float* Rb,
+                          const void* w, double lambda, float* psi_out, float* Ra,
+                          double* partials, bool write_pad, hipStream_t s) {
+    const unsigned grid = grid_for(g.My * g.Mz, kWaves);
+    if (st == Store::F32)
+        hipLaunchKernelGGL(k_update_pad<0>, dim3(grid), dim3(kBlock), 0, s, g, psi_in, Rb, w,
+                           lambda, psi_out, Ra, partials, int(write_pad));
+    else
+        hipLaunchKernelGGL(k_update_pad<1>, dim3(grid), dim3(kBlock), 0, s, g, psi_in, Rb, w,
+                           lambda, psi_out, Ra, partials, int(write_pad));
+    SD_HIP(hipGetLastError());
+    return grid;
+}
+
+void launch_reduce_partials(const double* partials, int64_t nblocks, double* out, int accumulate,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, s, partials, nblocks, out,
+                       accumulate);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_spec_mul(float* C, const float* K, int64_t n, hipStream_t s) {
+    const int64_t n2 = n / 2;
+    const int tail = int(n & 1);
+    const unsigned grid = grid_for(n2, kBlock, 256 * 32);
+    hipLaunchKernelGGL(k_spec_mul, dim3(grid), dim3(kBlock), 0, s, reinterpret_cast<float4*>(C),
+                       reinterpret_cast<const float4*>(K), n2,
+                       reinterpret_cast<float2*>(C) + (n - 1),
+                       reinterpret_cast<const float2*>(K) + (n - 1), tail);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_place_kernel(const SlabGeom& g, const float* k, int kx, int ky, int kz, float scale,
+                         float* R, hipStream_t s) {
+    SD_HIP(hipMemsetAsync(R, 0, size_t(g.Sx * g.My * g.Mz) * sizeof(float), s));
+    const int64_t n = int64_t(kx) * ky * kz;
+    hipLaunchKernelGGL(k_place_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, g, k, kx, ky, kz,
+                       scale, R);
+    SD_HIP(hipGetLastError());
+}
+
+int64_t launch_first_iteration(int64_t n, int nviews, Store st, const void* const* d_imgs,
+                               double* partials, hipStream_t s) {
+    const unsigned grid = grid_for(n, kBlock, 2048);
+    if (st == Store::F32)
+        hipLaunchKernelGGL(k_first_iteration<0>, dim3(grid), dim3(kBlock), 0, s, n, nviews, d_imgs,
+                           partials);
+    else
+        hipLaunchKernelGGL(k_first_iteration<1>, dim3(grid), dim3(kBlock), 0, s, n, nviews, d_imgs,
+                           partials);
+    SD_HIP(hipGetLastError());
+    return grid;
+}
+
+void launch_fill(float* p, int64_t n, float v, hipStream_t s) {
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_clamp_min(float* p, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_clamp_min, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_mask(float* psi, int64_t n, int nviews, Store st, const void* const* d_imgs,
+                 hipStream_t s) {
+    if (st == Store::F32)
+        hipLaunchKernelGGL(k_mask<0>, dim3(grid_for(n, 256)), dim3(256), 0, s, psi, n, nviews,
+                           d_imgs);
+    else
+        hipLaunchKernelGGL(k_mask<1>, dim3(grid_for(n, 256)), dim3(256), 0, s, psi, n, nviews,
+                           d_imgs);
+    SD_HIP(hipGetLastError());
+}
+
+void launch_to_half(const float* in, void* out, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_to_half, dim3(grid_for(n, 256)), dim3(256), 0, s, in,
+                       static_cast<__half*>(out), n);
+    SD_HIP(hipGetLastError());
+}
+
+}  // namespace spimdecon

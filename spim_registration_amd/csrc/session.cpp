@@ -1,0 +1,441 @@
+// session.cpp -- see session.hpp.
+#include "session.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace spimdecon {
+
+#define SD_NCCL(expr)                                                                          \
+    do {                                                                                       \
+        ncclResult_t _r = (expr);                                                              \
+        if (_r != ncclSuccess)                                                                 \
+            ::spimdecon::fail(SPIMDECON_ERR_COMM,                                              \
+                              std::string(#expr " failed: ") + ncclGetErrorString(_r));        \
+    } while (0)
+
+void slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1) {
+    const int64_t base = nz / nparts, rem = nz % nparts;
+    *z0 = int64_t(idx) * base + std::min<int64_t>(idx, rem);
+    *z1 = *z0 + base + (idx < rem ? 1 : 0);
+}
+
+Session::Session(const mvd_params& p) : p_(p) {
+    SD_CHECK(p.dims[0] >= 1 && p.dims[1] >= 1 && p.dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
+    SD_CHECK(p.local_slabs >= 1, SPIMDECON_ERR_ARG, "local_slabs must be >= 1");
+    SD_CHECK(p.local_slabs <= p.dims[2], SPIMDECON_ERR_ARG, "more slabs than z planes");
+    SD_CHECK(p.nranks >= 1 && p.rank >= 0 && p.rank < p.nranks, SPIMDECON_ERR_ARG, "bad rank");
+    SD_CHECK(p.ij_threads >= 1, SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
+    if (p_.nz_global <= 0) p_.nz_global = p.dims[2];
+    SD_CHECK(p_.z_offset >= 0 && p_.z_offset + p.dims[2] <= p_.nz_global, SPIMDECON_ERR_ARG,
+             "z range outside nz_global");
+    SD_CHECK(p_.nranks == 1 || p_.comm_id != nullptr, SPIMDECON_ERR_ARG,
+             "nranks > 1 needs comm_id");
+    check_device(p.device);
+    store_ = p.storage_fp16 ? Store::F16 : Store::F32;
+    DeviceGuard guard(p.device);
+    SD_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (p_.nranks > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, p_.comm_id, sizeof(id));
+        SD_NCCL(ncclCommInitRank(&comm_, p_.nranks, id, p_.rank));
+        p_.comm_id = nullptr;  // caller-owned; not retained
+    }
+    slabs_.resize(p.local_slabs);
+    for (int s = 0; s < p.local_slabs; ++s) {
+        int64_t a, b;
+        slab_range(p.dims[2], p.local_slabs, s, &a, &b);
+        SlabState& sl = slabs_[s];
+        sl.local_z0 = a;
+        sl.g.nx = p.dims[0];
+        sl.g.ny = p.dims[1];
+        sl.g.nz = b - a;
+        sl.g.z0 = p_.z_offset + a;
+        sl.g.nzg = p_.nz_global;
+        sl.n = sl.g.nx * sl.g.ny * sl.g.nz;
+    }
+}
+
+Session::~Session() {
+    DeviceGuard guard(p_.device);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& r : trecs_) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    for (auto e : event_pool_) (void)hipEventDestroy(e);
+    slabs_.clear();
+    stats_dev_.release();
+    if (comm_) ncclCommDestroy(comm_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Session::add_view(const float* img, const float* weight, const float* k1, const int* kdims,
+                       bool device_ptrs) {
+    SD_CHECK(img && weight && k1 && kdims, SPIMDECON_ERR_ARG, "null argument");
+    SD_CHECK(!spectra_ready_, SPIMDECON_ERR_STATE, "views must be added before mvd_init");
+    DeviceGuard guard(p_.device);
+    HostKernel hk;
+    for (int d = 0; d < 3; ++d) {
+        SD_CHECK(kdims[d] >= 1 && (kdims[d] & 1), SPIMDECON_ERR_ARG, "kernel dims must be odd");
+        hk.dims[d] = kdims[d];
+    }
+    hk.data.assign(k1, k1 + int64_t(kdims[0]) * kdims[1] * kdims[2]);
+    k1_.push_back(std::move(hk));
+    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const int64_t plane = p_.dims[0] * p_.dims[1];
+    DBuf<float> tmp;
+    for (auto& sl : slabs_) {
+        const size_t esz = store_ == Store::F32 ? 4 : 2;
+        for (int which = 0; which < 2; ++which) {
+            const float* src = (which == 0 ? img : weight) + sl.local_z0 * plane;
+            DBuf<char> buf(size_t(sl.n) * esz);
+            if (store_ == Store::F32) {
+                SD_HIP(hipMemcpyAsync(buf.p, src, size_t(sl.n) * 4, kind, stream_));
+            } else {
+                if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
+                SD_HIP(hipMemcpyAsync(tmp.p, src, size_t(sl.n) * 4, kind, stream_));
+                launch_to_half(tmp.p, buf.p, sl.n, stream_);
+            }
+            (which == 0 ? sl.img : sl.w).push_back(std::move(buf));
+        }
+    }
+    SD_HIP(hipStreamSynchronize(stream_));
+    ++nviews_;
+    kernels_ready_ = false;
+}
+
+void Session::init(int psftype) {
+    SD_CHECK(nviews_ >= 1, SPIMDECON_ERR_STATE, "no views added");
+    std::vector<HostKernel> k1 = k1_;
+    prepare_kernels_gpu(k1, k2_, psftype, p_.ij_threads, p_.device);
+    k1_ = std::move(k1);
+    kernels_ready_ = true;
+    build_spectra();
+}
+
+void Session::set_kernels(int view, const float* k1, const float* k2) {
+    SD_CHECK(view >= 0 && view < nviews_, SPIMDECON_ERR_ARG, "bad view index");
+    SD_CHECK(k1 && k2, SPIMDECON_ERR_ARG, "null kernel");
+    if (k2_.size() != size_t(nviews_)) k2_.resize(nviews_);
+    const int64_t n = int64_t(k1_[view].dims[0]) * k1_[view].dims[1] * k1_[view].dims[2];
+    k1_[view].data.assign(k1, k1 + n);
+    std::memcpy(k2_[view].dims, k1_[view].dims, sizeof(k1_[view].dims));
+    k2_[view].data.assign(k2, k2 + n);
+    spectra_ready_ = false;
+    bool all = true;
+    for (auto& k : k2_) all &= !k.data.empty();
+    if (all) {
+        kernels_ready_ = true;
+        build_spectra();
+    }
+}
+
+void Session::get_kernels(int view, float* k1, float* k2) const {
+    SD_CHECK(kernels_ready_, SPIMDECON_ERR_STATE, "kernels not prepared");
+    SD_CHECK(view >= 0 && view < nviews_, SPIMDECON_ERR_ARG, "bad view index");
+    if (k1) std::copy(k1_[view].data.begin(), k1_[view].data.end(), k1);
+    if (k2) std::copy(k2_[view].data.begin(), k2_[view].data.end(), k2);
+}
+
+void Session::build_spectra() {
+    DeviceGuard guard(p_.device);
+    int h[3] = {0, 0, 0};
+    for (int v = 0; v < nviews_; ++v)
+        for (int d = 0; d < 3; ++d) h[d] = std::max(h[d], k1_[v].dims[d] / 2);
+    for (int d = 0; d < 3; ++d) halo_[d] = std::max(h[d], p_.halo[d]);
+    const int total_slabs = p_.local_slabs * p_.nranks;
+    for (auto& sl : slabs_) {
+        SlabGeom& g = sl.g;
+        g.cx = halo_[0];
+        g.cy = halo_[1];
+        g.cz = halo_[2];
+        if (total_slabs > 1)
+            SD_CHECK(g.nz >= g.cz + 1, SPIMDECON_ERR_ARG,
+                     "slab thinner than kernel half size + 1 (" + std::to_string(g.nz) + " < " +
+                         std::to_string(g.cz + 1) + ")");
+        sl.pd.M[0] = fft_fast_size(g.nx + 2 * g.cx, true);
+        sl.pd.M[1] = fft_fast_size(g.ny + 2 * g.cy, false);
+        sl.pd.M[2] = fft_fast_size(g.nz + 2 * g.cz, false);
+        g.Mx = sl.pd.M[0];
+        g.My = sl.pd.M[1];
+        g.Mz = sl.pd.M[2];
+        g.Sx = sl.pd.Sx();
+        const size_t rf = size_t(sl.pd.real_floats());
+        sl.Ra.alloc(rf);
+        sl.Rb.alloc(rf);
+        sl.partials.alloc(2 * 256 * 16);
+        sl.fft.reset(new FftPlan3D());
+        sl.fft->create(sl.pd, stream_);
+        std::vector<const void*> ptrs(nviews_);
+        for (int v = 0; v < nviews_; ++v) ptrs[v] = sl.img[v].p;
+        sl.img_ptrs.alloc(nviews_);
+        SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
+                              hipMemcpyHostToDevice, stream_));
+        const float scale = float(1.0 / double(sl.pd.logical()));
+        sl.k1spec.clear();
+        sl.k2spec.clear();
+        DBuf<float> kd;
+        for (int v = 0; v < nviews_; ++v) {
+            for (int which = 0; which < 2; ++which) {
+                const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
+                kd.alloc(hk.data.size());
+                SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
+                DBuf<float> spec(rf);
+                launch_place_kernel(g, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p, stream_);
+                sl.fft->forward(spec.p);
+                SD_HIP(hipStreamSynchronize(stream_));
+                (which == 0 ? sl.k1spec : sl.k2spec).push_back(std::move(spec));
+            }
+        }
+    }
+    SD_HIP(hipStreamSynchronize(stream_));
+    spectra_ready_ = true;
+}
+
+double Session::init_psi(const float* psi_or_null) {
+    SD_CHECK(nviews_ >= 1, SPIMDECON_ERR_STATE, "no views added");
+    DeviceGuard guard(p_.device);
+    double avg = std::nan("");
+    for (auto& sl : slabs_) {
+        if (!sl.psi_a.p) {
+            sl.psi_a.alloc(sl.n);
+            sl.psi_b.alloc(sl.n);
+        }
+        sl.psi = sl.psi_a.p;
+        sl.psi_next = sl.psi_b.p;
+        if (sl.img_ptrs.n != size_t(nviews_)) {
+            std::vector<const void*> ptrs(nviews_);
+            for (int v = 0; v < nviews_; ++v) ptrs[v] = sl.img[v].p;
+            sl.img_ptrs.alloc(nviews_);
+            SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
+                                  hipMemcpyHostToDevice, stream_));
+        }
+    }
+    if (psi_or_null) {
+        const int64_t plane = p_.dims[0] * p_.dims[1];
+        for (auto& sl : slabs_) {
+            SD_HIP(hipMemcpyAsync(sl.psi, psi_or_null + sl.local_z0 * plane, size_t(sl.n) * 4,
+                                  hipMemcpyHostToDevice, stream_));
+            launch_clamp_min(sl.psi, sl.n, stream_);
+        }
+    } else {
+        // FirstIteration + fuseFirstIteration (MVDeconvolution.java:192-235)
+        double acc[2] = {0.0, 0.0};
+        std::vector<double> part;
+        for (auto& sl : slabs_) {
+            DBuf<double> dpart(2 * 2048);
+            const int64_t nb = launch_first_iteration(sl.n, nviews_, store_, sl.img_ptrs.p, dpart.p, stream_);
+            part.resize(2 * nb);
+            SD_HIP(hipMemcpyAsync(part.data(), dpart.p, part.size() * 8, hipMemcpyDeviceToHost, stream_));
+            SD_HIP(hipStreamSynchronize(stream_));
+            for (int64_t i = 0; i < nb; ++i) {
+                acc[0] += part[2 * i];
+                acc[1] += part[2 * i + 1];
+            }
+        }
+        allreduce_sum(acc, 2);
+        avg = acc[0] / acc[1];  // NaN when no voxel has data
+        const double a = std::isnan(avg) ? 0.5 : avg;  // :117-121
+        for (auto& sl : slabs_) launch_fill(sl.psi, sl.n, float(a), stream_);
+    }
+    SD_HIP(hipStreamSynchronize(stream_));
+    psi_ready_ = true;
+    return avg;
+}
+
+hipEvent_t Session::get_event() {
+    if (!event_pool_.empty()) {
+        hipEvent_t e = event_pool_.back();
+        event_pool_.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    SD_HIP(hipEventCreate(&e));
+    return e;
+}
+
+void Session::tstart(int cls) {
+    if (!timing_on_) return;
+    TimingRec r{cls, get_event(), nullptr};
+    SD_HIP(hipEventRecord(r.a, stream_));
+    trecs_.push_back(r);
+    tcur_ = int(trecs_.size()) - 1;
+}
+
+void Session::tstop() {
+    if (!timing_on_ || tcur_ < 0) return;
+    trecs_[tcur_].b = get_event();
+    SD_HIP(hipEventRecord(trecs_[tcur_].b, stream_));
+    tcur_ = -1;
+}
+
+void Session::timing(double* out16) {
+    for (int i = 0; i < 16; ++i) out16[i] = tacc_[i];
+}
+
+void Session::exchange(bool buffer_a) {
+    const size_t plane = size_t(slabs_[0].g.Sx * slabs_[0].g.My);
+    const int S = int(slabs_.size());
+    if (S == 1 && p_.nranks == 1) return;
+    tstart(5);
+    const int cz = halo_[2];
+    const size_t bytes = size_t(cz) * plane * sizeof(float);
+    auto buf = [&](SlabState& sl) { return buffer_a ? sl.Ra.p : sl.Rb.p; };
+    if (cz > 0) {
+        // local neighbours (virtual slabs on this device)
+        for (int s = 1; s < S; ++s) {
+            SlabState& lo = slabs_[s - 1];
+            SlabState& hi = slabs_[s];
+            // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
+            SD_HIP(hipMemcpyAsync(buf(lo) + size_t(lo.g.nz) * plane, buf(hi), bytes,
+                                  hipMemcpyDeviceToDevice, stream_));
+            // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
+            SD_HIP(hipMemcpyAsync(buf(hi) + size_t(hi.g.Mz - cz) * plane,
+                                  buf(lo) + size_t(lo.g.nz - cz) * plane, bytes,
+                                  hipMemcpyDeviceToDevice, stream_));
+        }
+        if (p_.nranks > 1) {
+            const size_t count = size_t(cz) * plane;
+            SD_NCCL(ncclGroupStart());
+            if (p_.rank > 0) {
+                SlabState& s0 = slabs_[0];
+                SD_NCCL(ncclSend(buf(s0), count, ncclFloat, p_.rank - 1, comm_, stream_));
+                SD_NCCL(ncclRecv(buf(s0) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
+                                 p_.rank - 1, comm_, stream_));
+            }
+            if (p_.rank < p_.nranks - 1) {
+                SlabState& sl = slabs_[S - 1];
+                SD_NCCL(ncclSend(buf(sl) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
+                                 p_.rank + 1, comm_, stream_));
+                SD_NCCL(ncclRecv(buf(sl) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
+                                 comm_, stream_));
+            }
+            SD_NCCL(ncclGroupEnd());
+        }
+    }
+    tstop();
+}
+
+void Session::allreduce_sum(double* host, int n) {
+    if (p_.nranks == 1) return;
+    DBuf<double> d(n);
+    SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
+    SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclSum, comm_, stream_));
+    SD_HIP(hipMemcpyAsync(host, d.p, n * 8, hipMemcpyDeviceToHost, stream_));
+    SD_HIP(hipStreamSynchronize(stream_));
+}
+
+void Session::allreduce_max(double* host, int n) {
+    if (p_.nranks == 1) return;
+    DBuf<double> d(n);
+    SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
+    SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclMax, comm_, stream_));
+    SD_HIP(hipMemcpyAsync(host, d.p, n * 8, hipMemcpyDeviceToHost, stream_));
+    SD_HIP(hipStreamSynchronize(stream_));
+}
+
+void Session::run(int iters, double lambda, double* stats) {
+    SD_CHECK(iters >= 0, SPIMDECON_ERR_ARG, "iters must be >= 0");
+    SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "call mvd_init (or mvd_set_kernels) first");
+    SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "call mvd_init_psi first");
+    DeviceGuard guard(p_.device);
+    if (iters == 0) return;
+    const int V = nviews_;
+    stats_dev_.alloc(size_t(iters) * V * 2);
+    // initial pad of psi for the first convolve1
+    for (auto& sl : slabs_) {
+        tstart(0);
+        launch_pad_mirror(sl.g, sl.psi, sl.Ra.p, stream_);
+        tstop();
+    }
+    exchange(true);
+    for (int it = 0; it < iters; ++it) {
+        for (int v = 0; v < V; ++v) {
+            const bool last = (it == iters - 1) && (v == V - 1);
+            for (auto& sl : slabs_) {                    // convolve1 + quotient
+                tstart(2); sl.fft->forward(sl.Ra.p); tstop();
+                tstart(3); launch_spec_mul(sl.Ra.p, sl.k1spec[v].p, sl.pd.complex_count(), stream_); tstop();
+                tstart(4); sl.fft->inverse(sl.Ra.p); tstop();
+                tstart(1); launch_quotient_pad(sl.g, store_, sl.img[v].p, sl.Ra.p, sl.Rb.p, stream_); tstop();
+            }
+            exchange(false);
+            for (size_t s = 0; s < slabs_.size(); ++s) {  // convolve2 + update
+                SlabState& sl = slabs_[s];
+                tstart(2); sl.fft->forward(sl.Rb.p); tstop();
+                tstart(3); launch_spec_mul(sl.Rb.p, sl.k2spec[v].p, sl.pd.complex_count(), stream_); tstop();
+                tstart(4); sl.fft->inverse(sl.Rb.p); tstop();
+                tstart(0);
+                const int64_t nb = launch_update_pad(sl.g, store_, sl.psi, sl.Rb.p, sl.w[v].p, lambda,
+                                                     sl.psi_next, sl.Ra.p, sl.partials.p, !last, stream_);
+                tstop();
+                tstart(6);
+                launch_reduce_partials(sl.partials.p, nb, stats_dev_.p + (size_t(it) * V + v) * 2,
+                                       s > 0 ? 1 : 0, stream_);
+                tstop();
+                std::swap(sl.psi, sl.psi_next);
+            }
+            if (!last) exchange(true);
+        }
+    }
+    std::vector<double> st(size_t(iters) * V * 2);
+    SD_HIP(hipMemcpyAsync(st.data(), stats_dev_.p, st.size() * 8, hipMemcpyDeviceToHost, stream_));
+    SD_HIP(hipStreamSynchronize(stream_));
+    if (p_.nranks > 1) {
+        std::vector<double> sums(size_t(iters) * V), maxs(size_t(iters) * V);
+        for (size_t i = 0; i < sums.size(); ++i) {
+            sums[i] = st[2 * i];
+            maxs[i] = st[2 * i + 1];
+        }
+        allreduce_sum(sums.data(), int(sums.size()));
+        allreduce_max(maxs.data(), int(maxs.size()));
+        for (size_t i = 0; i < sums.size(); ++i) {
+            st[2 * i] = sums[i];
+            st[2 * i + 1] = maxs[i];
+        }
+    }
+    if (stats) std::copy(st.begin(), st.end(), stats);
+    if (timing_on_) {
+        for (auto& r : trecs_) {
+            float ms = 0.f;
+            SD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            tacc_[r.cls] += ms;
+            tacc_[8 + r.cls] += 1.0;
+            event_pool_.push_back(r.a);
+            event_pool_.push_back(r.b);
+        }
+        trecs_.clear();
+    }
+}
+
+void Session::apply_mask() {
+    SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
+    DeviceGuard guard(p_.device);
+    for (auto& sl : slabs_) launch_mask(sl.psi, sl.n, nviews_, store_, sl.img_ptrs.p, stream_);
+    SD_HIP(hipStreamSynchronize(stream_));
+}
+
+void Session::get_psi(float* out) {
+    SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
+    SD_CHECK(out, SPIMDECON_ERR_ARG, "null output");
+    DeviceGuard guard(p_.device);
+    const int64_t plane = p_.dims[0] * p_.dims[1];
+    for (auto& sl : slabs_)
+        SD_HIP(hipMemcpyAsync(out + sl.local_z0 * plane, sl.psi, size_t(sl.n) * 4,
+                              hipMemcpyDeviceToHost, stream_));
+    SD_HIP(hipStreamSynchronize(stream_));
+}
+
+float* Session::psi_device(int slab) {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    return slabs_[slab].psi;
+}
+
+void Session::fft_dims(int slab, int64_t* out3) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
+    for (int d = 0; d < 3; ++d) out3[d] = slabs_[slab].pd.M[d];
+}
+
+}  // namespace spimdecon

@@ -1,0 +1,144 @@
+"""CPU, world_size 2 over gloo: the z-slab decomposition used by the multi-GPU
+path is exact.
+
+Each rank owns the slab ``mvd_slab_range`` (the C-ABI the GPU path uses)
+assigns it, exchanges ``c_z`` halo planes with its neighbour before each
+convolution exactly as libspimdecon's exchange does (psi before convolve1,
+the quotient before convolve2; mirror / constant-1 extension only at the
+global boundary), and all-reduces {sumChange (sum), maxChange (max)}.  The
+compute per slab is the oracle's; the gathered psi must equal the
+whole-volume oracle result, and the RCCL id broadcast helper must deliver
+rank 0's bytes to every rank.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import mvdecon_ref as ref
+from spim_registration_amd import synthetic
+from spim_registration_amd.distributed import broadcast_comm_id, halo_planes_needed, slab_range
+
+SHAPE = (30, 12, 14)      # z, y, x
+KS = (5, 5, 7)            # kx, ky, kz  -> cz = 3
+ITERS = 2
+LAM = 0.006
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _exchange(block, z0, z1, nz, cz, rank, world):
+    """block: local slab [z1-z0, y, x]; returns the slab with cz halo planes
+    from the neighbours (None where the global boundary is)."""
+    lower = upper = None
+    reqs = []
+    if rank > 0:
+        lower = torch.empty((cz,) + block.shape[1:], dtype=torch.float32)
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(block[:cz])), rank - 1))
+        reqs.append(dist.irecv(lower, rank - 1))
+    if rank < world - 1:
+        upper = torch.empty((cz,) + block.shape[1:], dtype=torch.float32)
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(block[-cz:])), rank + 1))
+        reqs.append(dist.irecv(upper, rank + 1))
+    for r in reqs:
+        r.wait()
+    return (lower.numpy() if lower is not None else None), (upper.numpy() if upper is not None else None)
+
+
+def _slab_conv(block, lower, upper, k, ext, cz):
+    """conv over the slab: neighbour planes where present, `ext` at the global ends."""
+    mode = {"mirror": "reflect", "one": "constant"}[ext]
+    kw = {"constant_values": 1.0} if ext == "one" else {}
+    pad_z_lo = lower if lower is not None else None
+    pad_z_hi = upper if upper is not None else None
+    ext_full = np.pad(block, [(cz, cz), (0, 0), (0, 0)], mode=mode, **kw)
+    if pad_z_lo is not None:
+        ext_full[:cz] = pad_z_lo
+    if pad_z_hi is not None:
+        ext_full[-cz:] = pad_z_hi
+    # x/y extension + valid convolution in z, x, y
+    out = ref.convolve(ext_full, k, ext)          # pads z again (ignored below)
+    return out[cz:-cz]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        imgs, ws, psfs, _ = synthetic.make_views(SHAPE, 2, config_id=21, ksize=KS,
+                                                 bead_density=1.0 / 5 ** 3)
+        k1s, k2s = ref.prepare_kernels(psfs, ref.PSFTYPE.OPTIMIZATION_I, 8)
+        nz = SHAPE[0]
+        cz = KS[2] // 2
+        z0, z1 = slab_range(nz, world, rank)
+        lo, up = halo_planes_needed(z0, z1, nz, cz)
+        assert (lo[1] - lo[0]) in (0, cz) and (up[1] - up[0]) in (0, cz)
+        # initial psi: global first-iteration average (all-reduced sums)
+        cnt, _ = ref.first_iteration([i[z0:z1] for i in imgs])
+        st = np.stack([i[z0:z1].astype(np.float64) for i in imgs])
+        pos = st > 0
+        c = pos.sum(0)
+        mean = np.where(c > 0, np.where(pos, st, 0).sum(0) / np.maximum(c, 1), 0)
+        acc = torch.tensor([mean[c > 0].sum(), float((c > 0).sum())], dtype=torch.float64)
+        dist.all_reduce(acc)
+        avg = float(acc[0] / acc[1])
+        psi = np.full((z1 - z0,) + SHAPE[1:], np.float32(avg), np.float32)
+        stats = []
+        for _ in range(ITERS):
+            for v in range(2):
+                l, u = _exchange(psi, z0, z1, nz, cz, rank, world)
+                blurred = _slab_conv(psi, l, u, k1s[v], "mirror", cz)
+                qt = ref.compute_quotient(blurred, imgs[v][z0:z1])
+                l, u = _exchange(qt, z0, z1, nz, cz, rank, world)
+                integ = _slab_conv(qt, l, u, k2s[v], "one", cz)
+                psi, s, m = ref.compute_final_values(psi, integ, ws[v][z0:z1], LAM)
+                t = torch.tensor([s], dtype=torch.float64)
+                mm = torch.tensor([m], dtype=torch.float64)
+                dist.all_reduce(t)
+                dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+                stats.append((float(t), float(mm)))
+        psi = np.where(cnt == 0, np.float32(0), psi).astype(np.float32)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (z0, psi))
+        cid = broadcast_comm_id(dist, rank, make_id=lambda: bytes(range(128)))
+        if rank == 0:
+            full = np.concatenate([g[1] for g in sorted(gathered, key=lambda g: g[0])])
+            res = ref.mv_deconvolution(imgs, ws, psfs, ref.PSFTYPE.OPTIMIZATION_I, ITERS, LAM)
+            err = float(np.linalg.norm(full - res.psi) / np.linalg.norm(res.psi))
+            serr = float(np.max(np.abs(np.array(stats) - np.array(res.stats).reshape(-1, 2)) /
+                                np.abs(np.array(res.stats).reshape(-1, 2))))
+            q.put(("ok", err, serr, cid == bytes(range(128))))
+        else:
+            q.put(("rank", rank, cid == bytes(range(128))))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put(("err", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_slab_decomposition_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [o for o in out if o[0] == "err"]
+    assert not errs, errs
+    ok = [o for o in out if o[0] == "ok"][0]
+    assert ok[1] < 1e-6, ok          # slab decomposition == whole volume
+    assert ok[2] < 1e-6, ok          # all-reduced per-view statistics
+    assert all(o[-1] for o in out)   # RCCL id broadcast delivered rank 0's bytes

@@ -1,0 +1,49 @@
+"""GPU parity of the DoG bead-detection pass against the oracle."""
+import numpy as np
+import pytest
+
+from oracle import dog_ref
+from spim_registration_amd import dog, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def bead_stack(shape=(40, 44, 48), cid=11):
+    rng = synthetic.rng_for(cid)
+    t = synthetic.truth_volume(shape, rng, bead_density=1.0 / 10 ** 3)
+    k = synthetic.psf(0, 1, (9, 9, 13), sigma=(1.0, 1.0, 1.6))
+    from oracle import mvdecon_ref as ref
+    img = ref.convolve(t.astype(np.float32), k, "mirror")
+    img = (rng.poisson(np.maximum(img * 2000 + 50, 0)) + rng.normal(0, 2, shape)).astype(np.float32)
+    return img
+
+
+@pytest.mark.parametrize("find_min,find_max", [(False, True), (True, True)])
+def test_dog_matches_oracle(gpu, find_min, find_max):
+    img = bead_stack()
+    pts, d = dog.compute(img, sigma=1.8, threshold=0.008, find_min=find_min, find_max=find_max,
+                         return_dog=True, keep_intensity=True)
+    exp, dref = dog_ref.process_dog(img, 1.8, 0.008, find_min=find_min, find_max=find_max)
+    # same float32 op order: bit-identical DoG image
+    np.testing.assert_array_equal(d, dref)
+    assert len(pts) == len(exp) and len(exp) > 10
+    got = [(int(p.location[0]), int(p.location[1]), int(p.location[2])) for p in pts]
+    assert got == [(e[0], e[1], e[2]) for e in exp]          # same order (x % T lists)
+    np.testing.assert_array_equal([p.intensity for p in pts], np.float32([e[3] for e in exp]))
+
+
+def test_dog_given_intensity_range(gpu):
+    img = bead_stack(shape=(24, 26, 30), cid=12)
+    pts, d = dog.compute(img, sigma=2.0, threshold=0.004, min_intensity=0.0, max_intensity=4000.0,
+                         return_dog=True)
+    exp, dref = dog_ref.process_dog(img, 2.0, 0.004, min_intensity=0.0, max_intensity=4000.0)
+    np.testing.assert_array_equal(d, dref)
+    assert [tuple(int(c) for c in p.location) for p in pts] == [e[:3] for e in exp]
+
+
+def test_dog_flat_image_has_no_peaks_and_no_nan(gpu):
+    img = np.full((12, 12, 12), 3.0, np.float32)   # min == max: normalisation skipped
+    pts, d = dog.compute(img, return_dog=True)
+    exp, dref = dog_ref.process_dog(img)
+    np.testing.assert_array_equal(d, dref)
+    assert len(pts) == len(exp)
