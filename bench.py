@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=256, help="edge of the CPU-baseline sample")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline pass")
+    ap.add_argument("--backend", default="engine", choices=["engine", "rocfft"])
     return ap.parse_args()
 
 
@@ -100,7 +101,8 @@ def main():
                                                 ksize=(args.ksize,) * 3, device=f"cuda:{local}")
     torch.cuda.synchronize()
     sess = Session((n, n, n), device=local, nranks=world, rank=rank, comm_id=comm_id,
-                   nz_global=nz_g, z_offset=rank * n, storage_fp16=args.fp16)
+                   nz_global=nz_g, z_offset=rank * n, storage_fp16=args.fp16,
+                   fft_backend=args.backend)
     for i, w, k in zip(imgs, ws, psfs):
         sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
     del imgs, ws

@@ -141,7 +141,8 @@ typedef struct mvd_params {
     int     fft_pad_policy; /* 0 = smallest 2^a3^b5^c7^d >= n+K-1 (default)        */
     int     halo[3];        /* max kernel half size {cx,cy,cz}; 0 = derive from views */
     int     ij_threads;     /* pinned reference thread count for the normImg quirk  */
-    int     reserved[8];
+    int     fft_backend;    /* 0 = fused spectral engine (default), 1 = rocFFT       */
+    int     reserved[7];
 } mvd_params;
 
 /* fills *p with defaults (local_slabs=1, nranks=1, ij_threads=8, ...) */

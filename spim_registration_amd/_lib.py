@@ -37,7 +37,8 @@ class MvdParams(C.Structure):
         ("fft_pad_policy", C.c_int),
         ("halo", C.c_int * 3),
         ("ij_threads", C.c_int),
-        ("reserved", C.c_int * 8),
+        ("fft_backend", C.c_int),
+        ("reserved", C.c_int * 7),
     ]
 
 

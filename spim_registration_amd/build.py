@@ -46,7 +46,7 @@ def _sources():
 
 
 def _headers():
-    return list(CSRC.glob("*.hpp")) + list(INCLUDE.glob("*.h"))
+    return list(CSRC.glob("*.hpp")) + list(CSRC.glob("*.inc")) + list(INCLUDE.glob("*.h"))
 
 
 def _stale(obj: Path, src: Path, hdr_mtime: float) -> bool:

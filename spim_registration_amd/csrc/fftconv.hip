@@ -1,0 +1,619 @@
+// fftconv.hip -- fused spectral-convolution engine (see fftconv.hpp).
+//
+// Semantics restated (paths under /root/reference/src/main/java/):
+//   convolve1 / convolve2   spim/process/fusion/deconvolution/MVDeconFFT.java:363-535
+//                           (true convolution, kernel centre at dim/2, extendMirrorSingle
+//                            for psi, extendValue(1) for the quotient)
+//   computeQuotient         spim/process/fusion/deconvolution/MVDeconvolution.java:473-525
+//   computeFinalValues      spim/process/fusion/deconvolution/MVDeconvolution.java:582-705
+#include "fftconv.hpp"
+
+#include <cmath>
+
+namespace spimdecon {
+
+namespace {
+
+// ------------------------------------------------------------------ small helpers
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// multiply by -i (forward) or +i (inverse)
+template <bool INV>
+__device__ __forceinline__ float2 mul_mi(float2 a) {
+    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+
+__device__ __forceinline__ int64_t s_of_q(int64_t q, int64_t n, int c, int64_t M) {
+    return q < n + c ? q : q - M;
+}
+__device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
+    if (n == 1) return 0;
+    const int64_t p = 2 * (n - 1);
+    int64_t j = s % p;
+    if (j < 0) j += p;
+    return j >= n ? p - j : j;
+}
+
+template <int S>
+__device__ __forceinline__ float ldv(const void* p, int64_t i) {
+    if constexpr (S == 0) return static_cast<const float*>(p)[i];
+    else return __half2float(static_cast<const __half*>(p)[i]);
+}
+
+// MVDeconvolution.computeNextValue (:671-703), float op order kept.
+__device__ __forceinline__ float next_value(float last, float integral, float weight, double lambda) {
+    const float value = __fmul_rn(last, integral);
+    float adjusted;
+    if (value > 0.0f) {
+        if (lambda > 0.0)
+            adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
+        else
+            adjusted = value;
+    } else {
+        adjusted = kMinValue;
+    }
+    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
+    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
+}
+
+// ------------------------------------------------------------------ radix-R DFTs
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft(float2* a) {
+    if constexpr (R == 2) {
+        const float2 t = a[0];
+        a[0] = cadd(t, a[1]);
+        a[1] = csub(t, a[1]);
+    } else if constexpr (R == 3) {
+        const float2 s = cadd(a[1], a[2]);
+        const float2 m = csub(a[0], cscale(s, 0.5f));
+        const float2 d = cscale(csub(a[1], a[2]), 0.86602540378443864676f);
+        a[0] = cadd(a[0], s);
+        const float2 id = mul_mi<INV>(d);  // -i*d forward
+        a[1] = cadd(m, id);
+        a[2] = csub(m, id);
+    } else if constexpr (R == 4) {
+        const float2 s0 = cadd(a[0], a[2]), d0 = csub(a[0], a[2]);
+        const float2 s1 = cadd(a[1], a[3]), d1 = mul_mi<INV>(csub(a[1], a[3]));
+        a[0] = cadd(s0, s1);
+        a[2] = csub(s0, s1);
+        a[1] = cadd(d0, d1);
+        a[3] = csub(d0, d1);
+    } else if constexpr (R == 5) {
+        constexpr float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+        constexpr float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+        const float2 b1 = cadd(a[1], a[4]), b2 = cadd(a[2], a[3]);
+        const float2 d1 = csub(a[1], a[4]), d2 = csub(a[2], a[3]);
+        const float2 m1 = cadd(a[0], cadd(cscale(b1, c1), cscale(b2, c2)));
+        const float2 m2 = cadd(a[0], cadd(cscale(b1, c2), cscale(b2, c1)));
+        const float2 n1 = mul_mi<INV>(cadd(cscale(d1, s1), cscale(d2, s2)));
+        const float2 n2 = mul_mi<INV>(csub(cscale(d1, s2), cscale(d2, s1)));
+        a[0] = cadd(a[0], cadd(b1, b2));
+        a[1] = cadd(m1, n1);
+        a[4] = csub(m1, n1);
+        a[2] = cadd(m2, n2);
+        a[3] = csub(m2, n2);
+    } else {
+        static_assert(R == 7, "radix 2, 3, 4, 5, 7 only");
+        constexpr float c1 = 0.62348980185873353053f, c2 = -0.22252093395631440429f,
+                        c3 = -0.90096886790241912624f;
+        constexpr float s1 = 0.78183148246802980871f, s2 = 0.97492791218182360702f,
+                        s3 = 0.43388373911755812048f;
+        const float2 b1 = cadd(a[1], a[6]), b2 = cadd(a[2], a[5]), b3 = cadd(a[3], a[4]);
+        const float2 d1 = csub(a[1], a[6]), d2 = csub(a[2], a[5]), d3 = csub(a[3], a[4]);
+        const float2 r1 = cadd(a[0], cadd(cscale(b1, c1), cadd(cscale(b2, c2), cscale(b3, c3))));
+        const float2 r2 = cadd(a[0], cadd(cscale(b1, c2), cadd(cscale(b2, c3), cscale(b3, c1))));
+        const float2 r3 = cadd(a[0], cadd(cscale(b1, c3), cadd(cscale(b2, c1), cscale(b3, c2))));
+        const float2 i1 = mul_mi<INV>(cadd(cscale(d1, s1), cadd(cscale(d2, s2), cscale(d3, s3))));
+        const float2 i2 = mul_mi<INV>(csub(cscale(d1, s2), cadd(cscale(d2, s3), cscale(d3, s1))));
+        const float2 i3 = mul_mi<INV>(cadd(csub(cscale(d1, s3), cscale(d2, s1)), cscale(d3, s2)));
+        a[0] = cadd(a[0], cadd(b1, cadd(b2, b3)));
+        a[1] = cadd(r1, i1);
+        a[6] = csub(r1, i1);
+        a[2] = cadd(r2, i2);
+        a[5] = csub(r2, i2);
+        a[3] = cadd(r3, i3);
+        a[4] = csub(r3, i3);
+    }
+}
+
+// One ping-pong Stockham stage: `ncols` interleaved transforms, element n of
+// column c at buf[n * ES + c * CS].  Thread (c, g) walks butterflies
+// j = g, g + TPC, ... of column c; one butterfly (R values) in registers at a time.
+template <int R, bool INV>
+__device__ __forceinline__ void stage_pp(const float2* __restrict__ src, float2* __restrict__ dst,
+                                         const float2* __restrict__ tw, int L, int Ns, int c, int g,
+                                         int TPC, int ES, int CS) {
+    const int nb = L / R;
+    const int step = L / (Ns * R);
+    for (int j = g; j < nb; j += TPC) {
+        const int k = j % Ns;
+        float2 v[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) v[t] = src[(j + t * nb) * ES + c * CS];
+        if (Ns > 1) {
+#pragma unroll
+            for (int t = 1; t < R; ++t) {
+                float2 w = tw[t * k * step];
+                if (INV) w.y = -w.y;
+                v[t] = cmul(v[t], w);
+            }
+        }
+        dft<R, INV>(v);
+        const int base = (j - k) * R + k;
+#pragma unroll
+        for (int t = 0; t < R; ++t) dst[(base + t * Ns) * ES + c * CS] = v[t];
+    }
+}
+
+// Full 1D FFT ping-ponging between a and b; returns the buffer holding the result.
+// Every stage ends with a block barrier (callers must call it uniformly).
+template <bool INV>
+__device__ __forceinline__ float2* fft_pp(float2* a, float2* b, const float2* tw, const Fft1D& f, int c, int g,
+                          int TPC, int ES, int CS, bool active) {
+    int Ns = 1;
+    float2* src = a;
+    float2* dst = b;
+    for (int s = 0; s < f.ns; ++s) {
+        const int R = f.radix(s);
+        if (active) {
+            switch (R) {
+                case 2: stage_pp<2, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
+                case 3: stage_pp<3, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
+                case 4: stage_pp<4, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
+                case 5: stage_pp<5, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
+                default: stage_pp<7, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
+            }
+        }
+        __syncthreads();
+        Ns *= R;
+        float2* t = src;
+        src = dst;
+        dst = t;
+    }
+    return src;
+}
+
+// ------------------------------------------------------------------ X pass (rows)
+
+enum XMode { XM_PSI = 0, XM_QUOT = 1, XM_UPDATE = 2, XM_KERNEL = 3 };
+
+struct XArgs {
+    SlabGeom g;
+    int64_t Hx, Hp;
+    Fft1D fx;
+    const int* row_mirror;
+    const int* row_one;
+    const float2* Cin;
+    float2* Cout;
+    const float* psi_in;
+    float* psi_out;
+    const void* img;
+    const void* w;
+    double lambda;
+    double* partials;
+    const float* kern;
+    int kx, ky, kz;
+    float kscale;
+};
+
+constexpr int kXThreads = 256;             // four waves; one packed row pair per wave
+constexpr int kXPairs = kXThreads / 64;
+
+// per-wave LDS: A[Mx + 2] | B[Mx + 2]; block: tw[Mx]
+__host__ __device__ inline int x_wave_elems(int Mx) { return 2 * (Mx + 2); }
+
+template <int MODE, int S>
+__global__ __launch_bounds__(kXThreads) void k_xpass(XArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    const SlabGeom& g = a.g;
+    const int Mx = int(g.Mx);
+    const int Hx = int(a.Hx);
+    const int Hp = int(a.Hp);
+    const int nx = int(g.nx);
+    const int cx = g.cx;
+    float2* tw = smem;
+    const int wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    float2* A = smem + Mx + wv * x_wave_elems(Mx);
+    float2* B = A + Mx + 2;
+    for (int i = threadIdx.x; i < Mx; i += kXThreads) tw[i] = a.fx.tw[i];
+    const int nrows = int(g.My * g.Mz);
+    const int npairs = (nrows + 1) / 2;
+    double ssum = 0.0;
+    float smax = -1.0f;
+    __syncthreads();
+    for (int pg = blockIdx.x; pg * kXPairs < npairs; pg += gridDim.x) {
+        const int pair = pg * kXPairs + wv;
+        const bool active = pair < npairs;
+        const int r0 = 2 * pair, r1 = 2 * pair + 1;
+        const bool valid0 = active && r0 < nrows, valid1 = active && r1 < nrows;
+        const int sm0 = valid0 ? a.row_mirror[r0] : -1, sm1 = valid1 ? a.row_mirror[r1] : -1;
+        const int so0 = valid0 ? a.row_one[r0] : -1, so1 = valid1 ? a.row_one[r1] : -1;
+        float2* Z = A;  // buffer holding the real-space row pair (x = row 0, y = row 1)
+        // ---------------- inverse half: previous convolution result
+        if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
+            int p0 = -1, p1 = -1;  // padded rows holding the needed convolution results
+            if constexpr (MODE == XM_QUOT) {
+                p0 = so0 >= 0 ? r0 : -1;
+                p1 = so1 >= 0 ? r1 : -1;
+            } else {
+                p0 = sm0 >= 0 ? (sm0 / int(g.ny)) * int(g.My) + sm0 % int(g.ny) : -1;
+                p1 = sm1 >= 0 ? (sm1 / int(g.ny)) * int(g.My) + sm1 % int(g.ny) : -1;
+            }
+            const float2* row0 = a.Cin + int64_t(p0) * Hp;
+            const float2* row1 = a.Cin + int64_t(p1) * Hp;
+            for (int k = lane; k < Hx; k += 64) {
+                B[k] = p0 >= 0 ? row0[k] : make_float2(0.f, 0.f);
+                B[Hx + k] = p1 >= 0 ? row1[k] : make_float2(0.f, 0.f);
+            }
+            __syncthreads();
+            for (int k = lane; k < Mx; k += 64) {
+                float2 xa, xb;
+                if (k <= Mx / 2) {
+                    xa = B[k];
+                    xb = B[Hx + k];
+                    if (k == 0 || k == Mx / 2) {
+                        xa.y = 0.f;
+                        xb.y = 0.f;
+                    }
+                } else {
+                    xa = B[Mx - k];
+                    xb = B[Hx + Mx - k];
+                    xa.y = -xa.y;
+                    xb.y = -xb.y;
+                }
+                A[k] = make_float2(xa.x - xb.y, xa.y + xb.x);
+            }
+            __syncthreads();
+            Z = fft_pp<true>(A, B, tw, a.fx, 0, lane, 64, 1, 0, active);
+        }
+        float2* O = (Z == A) ? B : A;  // the other buffer
+        // ---------------- pointwise: real rows -> Z (in place)
+        if constexpr (MODE == XM_PSI) {
+            const float* p0 = a.psi_in + int64_t(sm0 < 0 ? 0 : sm0) * nx;
+            const float* p1 = a.psi_in + int64_t(sm1 < 0 ? 0 : sm1) * nx;
+            for (int qx = lane; qx < Mx; qx += 64) {
+                const int sx = qx < nx + cx ? qx : qx - Mx;
+                const int lx = int(mirror_idx(sx, nx));
+                Z[qx] = make_float2(sm0 >= 0 ? p0[lx] : 0.f, sm1 >= 0 ? p1[lx] : 0.f);
+            }
+        } else if constexpr (MODE == XM_KERNEL) {
+            for (int qx = lane; qx < Mx; qx += 64) {
+                float v[2] = {0.f, 0.f};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int r = h == 0 ? r0 : r1;
+                    if (!(h == 0 ? valid0 : valid1)) continue;
+                    const int qz = r / int(g.My), qy = r % int(g.My);
+                    const int jz = (qz + a.kz / 2) % int(g.Mz), jy = (qy + a.ky / 2) % int(g.My);
+                    const int jx = (qx + a.kx / 2) % Mx;
+                    if (jz < a.kz && jy < a.ky && jx < a.kx)
+                        v[h] = a.kern[(int64_t(jz) * a.ky + jy) * a.kx + jx] * a.kscale;
+                }
+                Z[qx] = make_float2(v[0], v[1]);
+            }
+        } else if constexpr (MODE == XM_QUOT) {
+            const bool live0 = valid0 && sm0 != -1, live1 = valid1 && sm1 != -1;
+            for (int qx = lane; qx < Mx; qx += 64) {
+                const float2 bz = Z[qx];
+                float q0 = live0 ? 1.0f : 0.0f, q1 = live1 ? 1.0f : 0.0f;  // constant-1 extension
+                if (qx < nx) {
+                    if (so0 >= 0) {
+                        const float iv = ldv<S>(a.img, int64_t(so0) * nx + qx);
+                        if (iv > 0.0f) q0 = __fdiv_rn(iv, bz.x);
+                    }
+                    if (so1 >= 0) {
+                        const float iv = ldv<S>(a.img, int64_t(so1) * nx + qx);
+                        if (iv > 0.0f) q1 = __fdiv_rn(iv, bz.y);
+                    }
+                }
+                Z[qx] = make_float2(q0, q1);
+            }
+        } else {  // XM_UPDATE
+            for (int qx = lane; qx < nx; qx += 64) {
+                const float2 iz = Z[qx];
+                float o0 = 0.f, o1 = 0.f;
+                if (sm0 >= 0) {
+                    const int64_t vi = int64_t(sm0) * nx + qx;
+                    const float last = a.psi_in[vi];
+                    o0 = next_value(last, iz.x, ldv<S>(a.w, vi), a.lambda);
+                    if (so0 >= 0) {  // interior row: the one writer of psi_out
+                        a.psi_out[vi] = o0;
+                        const float ch = fabsf(__fsub_rn(o0, last));
+                        ssum += (double)ch;
+                        smax = fmaxf(smax, ch);
+                    }
+                }
+                if (sm1 >= 0) {
+                    const int64_t vi = int64_t(sm1) * nx + qx;
+                    const float last = a.psi_in[vi];
+                    o1 = next_value(last, iz.y, ldv<S>(a.w, vi), a.lambda);
+                    if (so1 >= 0) {
+                        a.psi_out[vi] = o1;
+                        const float ch = fabsf(__fsub_rn(o1, last));
+                        ssum += (double)ch;
+                        smax = fmaxf(smax, ch);
+                    }
+                }
+                Z[qx] = make_float2(o0, o1);
+            }
+            __syncthreads();
+            for (int qx = nx + lane; qx < Mx; qx += 64) {
+                const int sx = qx < nx + cx ? qx : qx - Mx;
+                Z[qx] = Z[mirror_idx(sx, nx)];
+            }
+        }
+        __syncthreads();
+        if (MODE == XM_UPDATE && a.Cout == nullptr) continue;
+        // ---------------- forward half
+        float2* F = fft_pp<false>(Z, O, tw, a.fx, 0, lane, 64, 1, 0, active);
+        const bool w0 = valid0 && sm0 != -1, w1 = valid1 && sm1 != -1;
+        float2* out0 = a.Cout + int64_t(r0) * Hp;
+        float2* out1 = a.Cout + int64_t(r1) * Hp;
+        for (int k = lane; k < Hp; k += 64) {
+            float2 xa = make_float2(0.f, 0.f), xb = make_float2(0.f, 0.f);
+            if (k < Hx) {
+                const float2 zk = F[k];
+                const float2 zm = F[k == 0 ? 0 : Mx - k];
+                xa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+                xb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+            }
+            if (w0) out0[k] = xa;
+            if (w1) out1[k] = xb;
+        }
+        __syncthreads();
+    }
+    if constexpr (MODE == XM_UPDATE) {
+        __shared__ double sh_sum[kXThreads / 64];
+        __shared__ float sh_max[kXThreads / 64];
+        for (int off = 32; off > 0; off >>= 1) {
+            ssum += __shfl_xor(ssum, off, 64);
+            smax = fmaxf(smax, __shfl_xor(smax, off, 64));
+        }
+        if (lane == 0) {
+            sh_sum[wv] = ssum;
+            sh_max[wv] = smax;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < kXThreads / 64; ++i) {
+                ssum += sh_sum[i];
+                smax = fmaxf(smax, sh_max[i]);
+            }
+            a.partials[2 * blockIdx.x] = ssum;
+            a.partials[2 * blockIdx.x + 1] = (double)smax;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ column passes
+
+constexpr int kCThreads = 1024;
+
+// dynamic LDS: A[L*TX] | B[L*TX] | tw[L]
+// AXIS 1 = y (stride Hp), 2 = z (stride My*Hp).  ZMODE: 0 = one FFT (fwd/inv by INV),
+// 1 = fwd * K * inv.
+#include "fftconv_col.inc"
+
+// ------------------------------------------------------------------ host side
+
+Fft1D make_fft(int L, DBuf<float2>& tw, hipStream_t s) {
+    Fft1D f;
+    f.L = L;
+    int m = L;
+    auto push = [&](int r) {
+        SD_CHECK(f.ns < kFftMaxStages, SPIMDECON_ERR_ARG, "too many FFT stages");
+        f.radix_packed |= uint64_t(r) << (4 * f.ns);
+        f.ns++;
+        m /= r;
+    };
+    while (m % 4 == 0) push(4);
+    while (m % 2 == 0) push(2);
+    while (m % 3 == 0) push(3);
+    while (m % 5 == 0) push(5);
+    while (m % 7 == 0) push(7);
+    SD_CHECK(m == 1, SPIMDECON_ERR_ARG, "FFT length " + std::to_string(L) + " is not 2,3,5,7-smooth");
+    std::vector<float2> h(L);
+    for (int i = 0; i < L; ++i) {
+        const double ang = -2.0 * M_PI * double(i) / double(L);
+        h[i] = make_float2(float(std::cos(ang)), float(std::sin(ang)));
+    }
+    tw.alloc(L);
+    SD_HIP(hipMemcpyAsync(tw.p, h.data(), L * sizeof(float2), hipMemcpyHostToDevice, s));
+    SD_HIP(hipStreamSynchronize(s));
+    f.tw = tw.p;
+    return f;
+}
+
+unsigned x_grid(const SpectralPlan& p) {
+    const int64_t npairs = (p.g.My * p.g.Mz + 1) / 2;
+    int64_t b = ceil_div(npairs, kXPairs);
+    return unsigned(std::min<int64_t>(b, 256 * 8));
+}
+
+size_t x_lds(const SpectralPlan& p) {
+    return size_t(p.g.Mx + kXPairs * x_wave_elems(int(p.g.Mx))) * sizeof(float2);
+}
+
+XArgs base_args(const SpectralPlan& p) {
+    XArgs a{};
+    a.g = p.g;
+    a.Hx = p.Hx;
+    a.Hp = p.Hp;
+    a.fx = p.fx;
+    a.row_mirror = p.row_mirror.p;
+    a.row_one = p.row_one.p;
+    return a;
+}
+
+template <int MODE>
+void launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+    const size_t lds = x_lds(p);
+    SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
+    SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
+    const unsigned grid = x_grid(p);
+    if (st == Store::F32) {
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xpass<MODE, 0>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+        hipLaunchKernelGGL((k_xpass<MODE, 0>), dim3(grid), dim3(kXThreads), lds, s, a);
+    } else {
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xpass<MODE, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+        hipLaunchKernelGGL((k_xpass<MODE, 1>), dim3(grid), dim3(kXThreads), lds, s, a);
+    }
+    SD_HIP(hipGetLastError());
+}
+
+int col_tx(int L) {
+    for (int tx : {16, 8, 4})
+        if (size_t(2 * L * tx + L) * sizeof(float2) <= 160 * 1024) return tx;
+    fail(SPIMDECON_ERR_ARG, "column FFT length " + std::to_string(L) + " exceeds the LDS tile");
+}
+
+template <int AXIS, bool INV, int ZMODE>
+void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+    const int tx = col_tx(f.L);
+    SD_CHECK(f.L * tx / 2 <= kColMaxU * kCThreads, SPIMDECON_ERR_ARG, "column tile exceeds prefetch registers");
+    const size_t lds = size_t(2 * f.L * tx + f.L) * sizeof(float2);
+    const int64_t ntiles = (p.Hp / tx) * (AXIS == 1 ? p.g.Mz : p.g.My);
+    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * (tx == 16 ? 1 : 2)));
+#define CL(TXV)                                                                                    \
+    case TXV:                                                                                      \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_colpass<AXIS, TXV, INV, ZMODE>), \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));         \
+        hipLaunchKernelGGL((k_colpass<AXIS, TXV, INV, ZMODE>), dim3(grid), dim3(kCThreads), lds, s, \
+                           p.g, p.Hp, f, C, K);                                                    \
+        break;
+    switch (tx) {
+        CL(16) CL(8) CL(4)
+        default: fail(SPIMDECON_ERR_ARG, "bad TX");
+    }
+#undef CL
+    SD_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+int64_t engine_fast_size(int64_t need, bool even) {
+    for (int64_t m = std::max<int64_t>(need, 1);; ++m) {
+        if (even && (m & 1)) continue;
+        int64_t r = m;
+        for (int64_t q : {2, 3, 5, 7})
+            while (r % q == 0) r /= q;
+        if (r == 1) return m;
+    }
+}
+
+void SpectralPlan::create(const SlabGeom& geom) {
+    g = geom;
+    SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");
+    Hx = g.Mx / 2 + 1;
+    Hp = ceil_div(Hx, 16) * 16;  // column tiles of 16 (or 8/4) complex stay 128-B aligned
+    hipStream_t s = nullptr;
+    fx = make_fft(int(g.Mx), twx, s);
+    fy = make_fft(int(g.My), twy, s);
+    fz = make_fft(int(g.Mz), twz, s);
+    const int64_t nrows = g.My * g.Mz;
+    std::vector<int> rm(nrows), ro(nrows);
+    auto mir = [](int64_t sidx, int64_t n) -> int64_t {
+        if (n == 1) return 0;
+        const int64_t p = 2 * (n - 1);
+        int64_t j = sidx % p;
+        if (j < 0) j += p;
+        return j >= n ? p - j : j;
+    };
+    for (int64_t qz = 0; qz < g.Mz; ++qz) {
+        const int64_t sz = qz < g.nz + g.cz ? qz : qz - g.Mz;
+        const int64_t gz = g.z0 + sz;
+        const bool gin = gz >= 0 && gz < g.nzg;
+        const bool skip = gin && (sz < 0 || sz >= g.nz);
+        const int64_t lz = mir(gz, g.nzg) - g.z0;
+        for (int64_t qy = 0; qy < g.My; ++qy) {
+            const int64_t r = qz * g.My + qy;
+            if (skip) {
+                rm[r] = ro[r] = -1;
+                continue;
+            }
+            SD_CHECK(lz >= 0 && lz < g.nz, SPIMDECON_ERR_ARG, "slab too thin for its mirror halo");
+            const int64_t sy = qy < g.ny + g.cy ? qy : qy - g.My;
+            const int64_t ly = mir(sy, g.ny);
+            rm[r] = int(lz * g.ny + ly);
+            const bool interior = (sz >= 0 && sz < g.nz) && (sy >= 0 && sy < g.ny);
+            ro[r] = interior ? int(sz * g.ny + sy) : -2;
+        }
+    }
+    row_mirror.alloc(nrows);
+    row_one.alloc(nrows);
+    SD_HIP(hipMemcpy(row_mirror.p, rm.data(), nrows * sizeof(int), hipMemcpyHostToDevice));
+    SD_HIP(hipMemcpy(row_one.p, ro.data(), nrows * sizeof(int), hipMemcpyHostToDevice));
+}
+
+void engine_forward_psi(const SpectralPlan& p, const float* psi, float2* C, hipStream_t s) {
+    XArgs a = base_args(p);
+    a.psi_in = psi;
+    a.Cout = C;
+    launch_x<XM_PSI>(a, Store::F32, p, s);
+}
+
+void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz,
+                            float scale, float2* Kspec, hipStream_t s) {
+    XArgs a = base_args(p);
+    // every padded row is a data row for the kernel (no mirror / skip semantics)
+    a.Cout = Kspec;
+    a.kern = d_kernel;
+    a.kx = kx;
+    a.ky = ky;
+    a.kz = kz;
+    a.kscale = scale;
+    // temporarily use a map that marks all rows valid: row_mirror >= 0 is all we test
+    DBuf<int> all(size_t(p.g.My * p.g.Mz));
+    SD_HIP(hipMemsetAsync(all.p, 0, all.bytes(), s));
+    a.row_mirror = all.p;
+    a.row_one = all.p;
+    launch_x<XM_KERNEL>(a, Store::F32, p, s);
+    launch_col<1, false, 0>(p, p.fy, Kspec, nullptr, s);
+    launch_col<2, false, 0>(p, p.fz, Kspec, nullptr, s);
+    SD_HIP(hipStreamSynchronize(s));
+}
+
+void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
+    if (inv) launch_col<1, true, 0>(p, p.fy, C, nullptr, s);
+    else launch_col<1, false, 0>(p, p.fy, C, nullptr, s);
+}
+
+void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s) {
+    if (K) launch_col<2, false, 1>(p, p.fz, C, K, s);
+    else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
+}
+
+void engine_quotient(const SpectralPlan& p, Store st, const float2* Cin, const void* img,
+                     float2* Cout, hipStream_t s) {
+    XArgs a = base_args(p);
+    a.Cin = Cin;
+    a.Cout = Cout;
+    a.img = img;
+    launch_x<XM_QUOT>(a, st, p, s);
+}
+
+int64_t engine_update(const SpectralPlan& p, Store st, const float2* Cin, const float* psi_in,
+                      const void* w, double lambda, float* psi_out, float2* Cout, double* partials,
+                      hipStream_t s) {
+    XArgs a = base_args(p);
+    a.Cin = Cin;
+    a.Cout = Cout;
+    a.psi_in = psi_in;
+    a.psi_out = psi_out;
+    a.w = w;
+    a.lambda = lambda;
+    a.partials = partials;
+    launch_x<XM_UPDATE>(a, st, p, s);
+    return x_grid(p);
+}
+
+}  // namespace spimdecon

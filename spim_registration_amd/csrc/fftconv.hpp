@@ -1,0 +1,77 @@
+// fftconv.hpp -- fused spectral-convolution engine for the RL iteration (MI355X).
+//
+// rocFFT runs a 540^3 R2C at ~8x the cost of one HBM pass (profiles/r01_*); this
+// engine instead streams the padded volume through five HBM passes per
+// convolution and fuses every pointwise step of the RL update into them:
+//
+//   X pass (rows, contiguous)      inverse real FFT of the previous convolution
+//                                  -> pointwise (quotient | Tikhonov update)
+//                                  -> forward real FFT of the next operand
+//   Y pass (columns, stride Hp)    complex FFT along y          (fwd / inv)
+//   Z pass (columns, stride My*Hp) FFT along z * kernel spectrum * inverse FFT
+//
+// Spectrum layout C[qz][qy][kx] (float2, row pitch Hp = Hx rounded to 16,
+// Hx = Mx/2 + 1).  Two real rows are transformed as one complex row (real /
+// imaginary parts) and split into their half spectra.  All 1D FFTs are
+// mixed-radix Stockham (radix 2, 3, 4, 5, 7) in LDS with a float twiddle
+// table computed in double.  Both directions are unnormalised; 1/(Mx*My*Mz) is
+// folded into the kernel spectra.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "common.hpp"
+#include "rl_kernels.hpp"
+
+namespace spimdecon {
+
+constexpr int kFftMaxStages = 16;
+
+struct Fft1D {
+    int L = 0;
+    int ns = 0;
+    uint64_t radix_packed = 0;   // radix of stage s in bits [4s, 4s+4) (no indexed array:
+                                 // a dynamically indexed kernel-argument array goes to scratch)
+    const float2* tw = nullptr;  // device table exp(-2*pi*i*m/L), m < L
+    __host__ __device__ int radix(int s) const { return int((radix_packed >> (4 * s)) & 15u); }
+};
+
+// per-slab engine state (twiddles, row maps)
+struct SpectralPlan {
+    SlabGeom g{};
+    int64_t Hx = 0, Hp = 0;
+    Fft1D fx, fy, fz;
+    DBuf<float2> twx, twy, twz;
+    DBuf<int> row_mirror;  // [My*Mz] local source row (lz*ny+ly) of the mirror extension; -1 skip
+    DBuf<int> row_one;     // [My*Mz] own local row if interior; -2 constant 1; -1 skip
+    int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
+    void create(const SlabGeom& geom);
+};
+
+// smallest M >= need whose factors are all in {2,3,5,7} and that the engine
+// supports (even when `even`)
+int64_t engine_fast_size(int64_t need, bool even);
+
+// ---- passes (all asynchronous on `s`) ----
+// psi -> C (x-spectra of the mirror-extended psi rows)
+void engine_forward_psi(const SpectralPlan& p, const float* psi, float2* C, hipStream_t s);
+// small kernel (kx,ky,kz) -> full 3D spectrum in Kspec (scaled), uses `work` as scratch-free in place
+void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz,
+                            float scale, float2* Kspec, hipStream_t s);
+// Y pass: in-place complex FFT along y (inverse when inv)
+void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
+// Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
+void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
+// X pass A: conv1 result (Cin) -> quotient with img -> forward spectrum into Cout
+void engine_quotient(const SpectralPlan& p, Store st, const float2* Cin, const void* img,
+                     float2* Cout, hipStream_t s);
+// X pass B: conv2 result (Cin) -> update psi_in -> psi_out, forward spectrum of the
+// mirror-extended psi_out into Cout (when Cout != nullptr); stats partials (2 doubles / block).
+// returns the number of partials written
+int64_t engine_update(const SpectralPlan& p, Store st, const float2* Cin, const float* psi_in,
+                      const void* w, double lambda, float* psi_out, float2* Cout, double* partials,
+                      hipStream_t s);
+
+}  // namespace spimdecon

@@ -34,6 +34,8 @@ Session::Session(const mvd_params& p) : p_(p) {
              "nranks > 1 needs comm_id");
     check_device(p.device);
     store_ = p.storage_fp16 ? Store::F16 : Store::F32;
+    backend_ = p.fft_backend;
+    SD_CHECK(backend_ == 0 || backend_ == 1, SPIMDECON_ERR_ARG, "unknown fft_backend");
     DeviceGuard guard(p.device);
     SD_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (p_.nranks > 1) {
@@ -155,38 +157,60 @@ void Session::build_spectra() {
             SD_CHECK(g.nz >= g.cz + 1, SPIMDECON_ERR_ARG,
                      "slab thinner than kernel half size + 1 (" + std::to_string(g.nz) + " < " +
                          std::to_string(g.cz + 1) + ")");
-        sl.pd.M[0] = fft_fast_size(g.nx + 2 * g.cx, true);
-        sl.pd.M[1] = fft_fast_size(g.ny + 2 * g.cy, false);
-        sl.pd.M[2] = fft_fast_size(g.nz + 2 * g.cz, false);
+        sl.pd.M[0] = engine_fast_size(g.nx + 2 * g.cx, true);
+        sl.pd.M[1] = engine_fast_size(g.ny + 2 * g.cy, false);
+        sl.pd.M[2] = engine_fast_size(g.nz + 2 * g.cz, false);
         g.Mx = sl.pd.M[0];
         g.My = sl.pd.M[1];
         g.Mz = sl.pd.M[2];
         g.Sx = sl.pd.Sx();
-        const size_t rf = size_t(sl.pd.real_floats());
-        sl.Ra.alloc(rf);
-        sl.Rb.alloc(rf);
         sl.partials.alloc(2 * 256 * 16);
-        sl.fft.reset(new FftPlan3D());
-        sl.fft->create(sl.pd, stream_);
         std::vector<const void*> ptrs(nviews_);
         for (int v = 0; v < nviews_; ++v) ptrs[v] = sl.img[v].p;
         sl.img_ptrs.alloc(nviews_);
         SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
                               hipMemcpyHostToDevice, stream_));
         const float scale = float(1.0 / double(sl.pd.logical()));
-        sl.k1spec.clear();
-        sl.k2spec.clear();
         DBuf<float> kd;
-        for (int v = 0; v < nviews_; ++v) {
-            for (int which = 0; which < 2; ++which) {
-                const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
-                kd.alloc(hk.data.size());
-                SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
-                DBuf<float> spec(rf);
-                launch_place_kernel(g, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p, stream_);
-                sl.fft->forward(spec.p);
-                SD_HIP(hipStreamSynchronize(stream_));
-                (which == 0 ? sl.k1spec : sl.k2spec).push_back(std::move(spec));
+        if (backend_ == 1) {
+            const size_t rf = size_t(sl.pd.real_floats());
+            sl.Ra.alloc(rf);
+            sl.Rb.alloc(rf);
+            sl.fft.reset(new FftPlan3D());
+            sl.fft->create(sl.pd, stream_);
+            sl.k1spec.clear();
+            sl.k2spec.clear();
+            for (int v = 0; v < nviews_; ++v) {
+                for (int which = 0; which < 2; ++which) {
+                    const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
+                    kd.alloc(hk.data.size());
+                    SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
+                    DBuf<float> spec(rf);
+                    launch_place_kernel(g, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p, stream_);
+                    sl.fft->forward(spec.p);
+                    SD_HIP(hipStreamSynchronize(stream_));
+                    (which == 0 ? sl.k1spec : sl.k2spec).push_back(std::move(spec));
+                }
+            }
+        } else {
+            sl.sp.create(g);
+            const size_t ne = size_t(sl.sp.spectrum_elems());
+            sl.C1.alloc(ne);
+            sl.C2.alloc(ne);
+            SD_HIP(hipMemsetAsync(sl.C1.p, 0, sl.C1.bytes(), stream_));
+            SD_HIP(hipMemsetAsync(sl.C2.p, 0, sl.C2.bytes(), stream_));
+            sl.e1spec.clear();
+            sl.e2spec.clear();
+            for (int v = 0; v < nviews_; ++v) {
+                for (int which = 0; which < 2; ++which) {
+                    const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
+                    kd.alloc(hk.data.size());
+                    SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
+                    DBuf<float2> spec(ne);
+                    engine_kernel_spectrum(sl.sp, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p,
+                                           stream_);
+                    (which == 0 ? sl.e1spec : sl.e2spec).push_back(std::move(spec));
+                }
             }
         }
     }
@@ -276,44 +300,52 @@ void Session::timing(double* out16) {
 }
 
 void Session::exchange(bool buffer_a) {
-    const size_t plane = size_t(slabs_[0].g.Sx * slabs_[0].g.My);
+    if (backend_ == 1) {
+        exchange_planes([](SlabState& sl, bool a) { return a ? sl.Ra.p : sl.Rb.p; }, buffer_a,
+                        size_t(slabs_[0].g.Sx * slabs_[0].g.My));
+    } else {
+        exchange_planes(
+            [](SlabState& sl, bool a) { return reinterpret_cast<float*>(a ? sl.C1.p : sl.C2.p); },
+            buffer_a, size_t(2 * slabs_[0].sp.Hp * slabs_[0].g.My));
+    }
+}
+
+// halo exchange of cz padded z-planes between neighbouring slabs (local copies and RCCL)
+void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane) {
     const int S = int(slabs_.size());
     if (S == 1 && p_.nranks == 1) return;
-    tstart(5);
     const int cz = halo_[2];
+    if (cz <= 0) return;
+    tstart(5);
     const size_t bytes = size_t(cz) * plane * sizeof(float);
-    auto buf = [&](SlabState& sl) { return buffer_a ? sl.Ra.p : sl.Rb.p; };
-    if (cz > 0) {
-        // local neighbours (virtual slabs on this device)
-        for (int s = 1; s < S; ++s) {
-            SlabState& lo = slabs_[s - 1];
-            SlabState& hi = slabs_[s];
-            // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
-            SD_HIP(hipMemcpyAsync(buf(lo) + size_t(lo.g.nz) * plane, buf(hi), bytes,
-                                  hipMemcpyDeviceToDevice, stream_));
-            // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
-            SD_HIP(hipMemcpyAsync(buf(hi) + size_t(hi.g.Mz - cz) * plane,
-                                  buf(lo) + size_t(lo.g.nz - cz) * plane, bytes,
-                                  hipMemcpyDeviceToDevice, stream_));
+    for (int s = 1; s < S; ++s) {
+        SlabState& lo = slabs_[s - 1];
+        SlabState& hi = slabs_[s];
+        // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
+        SD_HIP(hipMemcpyAsync(get(lo, which) + size_t(lo.g.nz) * plane, get(hi, which), bytes,
+                              hipMemcpyDeviceToDevice, stream_));
+        // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
+        SD_HIP(hipMemcpyAsync(get(hi, which) + size_t(hi.g.Mz - cz) * plane,
+                              get(lo, which) + size_t(lo.g.nz - cz) * plane, bytes,
+                              hipMemcpyDeviceToDevice, stream_));
+    }
+    if (p_.nranks > 1) {
+        const size_t count = size_t(cz) * plane;
+        SD_NCCL(ncclGroupStart());
+        if (p_.rank > 0) {
+            SlabState& s0 = slabs_[0];
+            SD_NCCL(ncclSend(get(s0, which), count, ncclFloat, p_.rank - 1, comm_, stream_));
+            SD_NCCL(ncclRecv(get(s0, which) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
+                             p_.rank - 1, comm_, stream_));
         }
-        if (p_.nranks > 1) {
-            const size_t count = size_t(cz) * plane;
-            SD_NCCL(ncclGroupStart());
-            if (p_.rank > 0) {
-                SlabState& s0 = slabs_[0];
-                SD_NCCL(ncclSend(buf(s0), count, ncclFloat, p_.rank - 1, comm_, stream_));
-                SD_NCCL(ncclRecv(buf(s0) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
-                                 p_.rank - 1, comm_, stream_));
-            }
-            if (p_.rank < p_.nranks - 1) {
-                SlabState& sl = slabs_[S - 1];
-                SD_NCCL(ncclSend(buf(sl) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
-                                 p_.rank + 1, comm_, stream_));
-                SD_NCCL(ncclRecv(buf(sl) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
-                                 comm_, stream_));
-            }
-            SD_NCCL(ncclGroupEnd());
+        if (p_.rank < p_.nranks - 1) {
+            SlabState& sl = slabs_[S - 1];
+            SD_NCCL(ncclSend(get(sl, which) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
+                             p_.rank + 1, comm_, stream_));
+            SD_NCCL(ncclRecv(get(sl, which) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
+                             comm_, stream_));
         }
+        SD_NCCL(ncclGroupEnd());
     }
     tstop();
 }
@@ -344,7 +376,40 @@ void Session::run(int iters, double lambda, double* stats) {
     if (iters == 0) return;
     const int V = nviews_;
     stats_dev_.alloc(size_t(iters) * V * 2);
-    // initial pad of psi for the first convolve1
+    if (backend_ == 1) run_rocfft(iters, lambda);
+    else run_engine(iters, lambda);
+    std::vector<double> st(size_t(iters) * V * 2);
+    SD_HIP(hipMemcpyAsync(st.data(), stats_dev_.p, st.size() * 8, hipMemcpyDeviceToHost, stream_));
+    SD_HIP(hipStreamSynchronize(stream_));
+    if (p_.nranks > 1) {
+        std::vector<double> sums(size_t(iters) * V), maxs(size_t(iters) * V);
+        for (size_t i = 0; i < sums.size(); ++i) {
+            sums[i] = st[2 * i];
+            maxs[i] = st[2 * i + 1];
+        }
+        allreduce_sum(sums.data(), int(sums.size()));
+        allreduce_max(maxs.data(), int(maxs.size()));
+        for (size_t i = 0; i < sums.size(); ++i) {
+            st[2 * i] = sums[i];
+            st[2 * i + 1] = maxs[i];
+        }
+    }
+    if (stats) std::copy(st.begin(), st.end(), stats);
+    if (timing_on_) {
+        for (auto& r : trecs_) {
+            float ms = 0.f;
+            SD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            tacc_[r.cls] += ms;
+            tacc_[8 + r.cls] += 1.0;
+            event_pool_.push_back(r.a);
+            event_pool_.push_back(r.b);
+        }
+        trecs_.clear();
+    }
+}
+
+void Session::run_rocfft(int iters, double lambda) {
+    const int V = nviews_;
     for (auto& sl : slabs_) {
         tstart(0);
         launch_pad_mirror(sl.g, sl.psi, sl.Ra.p, stream_);
@@ -379,33 +444,46 @@ void Session::run(int iters, double lambda, double* stats) {
             if (!last) exchange(true);
         }
     }
-    std::vector<double> st(size_t(iters) * V * 2);
-    SD_HIP(hipMemcpyAsync(st.data(), stats_dev_.p, st.size() * 8, hipMemcpyDeviceToHost, stream_));
-    SD_HIP(hipStreamSynchronize(stream_));
-    if (p_.nranks > 1) {
-        std::vector<double> sums(size_t(iters) * V), maxs(size_t(iters) * V);
-        for (size_t i = 0; i < sums.size(); ++i) {
-            sums[i] = st[2 * i];
-            maxs[i] = st[2 * i + 1];
-        }
-        allreduce_sum(sums.data(), int(sums.size()));
-        allreduce_max(maxs.data(), int(maxs.size()));
-        for (size_t i = 0; i < sums.size(); ++i) {
-            st[2 * i] = sums[i];
-            st[2 * i + 1] = maxs[i];
-        }
+}
+
+// timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 fused z pass,
+// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce
+void Session::run_engine(int iters, double lambda) {
+    const int V = nviews_;
+    for (auto& sl : slabs_) {
+        tstart(4);
+        engine_forward_psi(sl.sp, sl.psi, sl.C1.p, stream_);
+        tstop();
     }
-    if (stats) std::copy(st.begin(), st.end(), stats);
-    if (timing_on_) {
-        for (auto& r : trecs_) {
-            float ms = 0.f;
-            SD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
-            tacc_[r.cls] += ms;
-            tacc_[8 + r.cls] += 1.0;
-            event_pool_.push_back(r.a);
-            event_pool_.push_back(r.b);
+    exchange(true);
+    for (int it = 0; it < iters; ++it) {
+        for (int v = 0; v < V; ++v) {
+            const bool last = (it == iters - 1) && (v == V - 1);
+            for (auto& sl : slabs_) {                    // convolve1 + quotient
+                tstart(2); engine_ypass(sl.sp, sl.C1.p, false, stream_); tstop();
+                tstart(3); engine_zpass(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_); tstop();
+                tstart(2); engine_ypass(sl.sp, sl.C1.p, true, stream_); tstop();
+                tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, stream_); tstop();
+            }
+            exchange(false);
+            for (size_t s = 0; s < slabs_.size(); ++s) {  // convolve2 + update (+ next forward x)
+                SlabState& sl = slabs_[s];
+                tstart(2); engine_ypass(sl.sp, sl.C2.p, false, stream_); tstop();
+                tstart(3); engine_zpass(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_); tstop();
+                tstart(2); engine_ypass(sl.sp, sl.C2.p, true, stream_); tstop();
+                tstart(0);
+                const int64_t nb = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda,
+                                                 sl.psi_next, last ? nullptr : sl.C1.p, sl.partials.p,
+                                                 stream_);
+                tstop();
+                tstart(6);
+                launch_reduce_partials(sl.partials.p, nb, stats_dev_.p + (size_t(it) * V + v) * 2,
+                                       s > 0 ? 1 : 0, stream_);
+                tstop();
+                std::swap(sl.psi, sl.psi_next);
+            }
+            if (!last) exchange(true);
         }
-        trecs_.clear();
     }
 }
 

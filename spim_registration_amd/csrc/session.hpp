@@ -20,6 +20,7 @@
 
 #include "common.hpp"
 #include "fft.hpp"
+#include "fftconv.hpp"
 #include "kernel_prep.hpp"
 #include "rl_kernels.hpp"
 
@@ -35,7 +36,10 @@ struct SlabState {
     float* psi_next = nullptr;
     std::vector<DBuf<char>> img, w;
     std::vector<DBuf<float>> k1spec, k2spec;
-    DBuf<float> Ra, Rb;
+    DBuf<float> Ra, Rb;                       // rocFFT backend work volumes
+    SpectralPlan sp;                           // engine backend
+    DBuf<float2> C1, C2;
+    std::vector<DBuf<float2>> e1spec, e2spec;
     DBuf<double> partials;
     DBuf<const void*> img_ptrs;
     std::unique_ptr<FftPlan3D> fft;
@@ -69,12 +73,16 @@ public:
 private:
     void build_spectra();
     void exchange(bool buffer_a);
+    void exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane_floats);
+    void run_rocfft(int iters, double lambda);
+    void run_engine(int iters, double lambda);
     void allreduce_sum(double* host, int n);
     void allreduce_max(double* host, int n);
     void tstart(int cls);
     void tstop();
 
     mvd_params p_{};
+    int backend_ = 0;  // 0 = fused spectral engine, 1 = rocFFT (mvd_params.fft_backend)
     Store store_ = Store::F32;
     hipStream_t stream_ = nullptr;
     ncclComm_t comm_ = nullptr;

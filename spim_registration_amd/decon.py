@@ -139,7 +139,8 @@ class Session:
     """Thin RAII wrapper of an ``mvd_session`` (GPU-resident RL state)."""
 
     def __init__(self, dims_xyz, device=0, local_slabs=1, nranks=1, rank=0, comm_id=None,
-                 nz_global=None, z_offset=0, storage_fp16=False, ij_threads=8, halo=None):
+                 nz_global=None, z_offset=0, storage_fp16=False, ij_threads=8, halo=None,
+                 fft_backend="engine"):
         self.lib = _lib.load()
         p = _lib.MvdParams()
         self.lib.mvd_params_default(C.byref(p))
@@ -155,6 +156,7 @@ class Session:
         p.comm_id = comm_id
         p.storage_fp16 = int(bool(storage_fp16))
         p.ij_threads = int(ij_threads)
+        p.fft_backend = {"engine": 0, "rocfft": 1}[fft_backend]
         if halo is not None:
             for d in range(3):
                 p.halo[d] = int(halo[d])
