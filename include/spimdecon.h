@@ -138,7 +138,10 @@ typedef struct mvd_params {
     int     rank;
     const char* comm_id;    /* 128-byte RCCL unique id (NULL when nranks == 1)     */
     int     storage_fp16;   /* 1: img/weights stored as fp16 (config-5 mode)       */
-    int     fft_pad_policy; /* 0 = smallest 2^a3^b5^c7^d >= n+K-1 (default)        */
+    int     fft_pad_policy; /* padded FFT length per axis (>= n + K - 1):            *
+                             * 0 = auto (two-factor fast-path length when within    *
+                             *     25% of the smallest 2,3,5,7-smooth length),      *
+                             * 1 = fast-path table only, 2 = smallest smooth length */
     int     halo[3];        /* max kernel half size {cx,cy,cz}; 0 = derive from views */
     int     ij_threads;     /* pinned reference thread count for the normImg quirk  */
     int     fft_backend;    /* 0 = fused spectral engine (default), 1 = rocFFT       */

@@ -28,9 +28,6 @@ __device__ __forceinline__ float2 mul_mi(float2 a) {
     return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
 
-__device__ __forceinline__ int64_t s_of_q(int64_t q, int64_t n, int c, int64_t M) {
-    return q < n + c ? q : q - M;
-}
 __device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
     if (n == 1) return 0;
     const int64_t p = 2 * (n - 1);
@@ -151,9 +148,18 @@ __device__ __forceinline__ void stage_pp(const float2* __restrict__ src, float2*
     }
 }
 
+// LDS hand-off between the lanes of one wave (a wave's LDS operations execute
+// in order; this only stops the compiler from moving them across).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Full 1D FFT ping-ponging between a and b; returns the buffer holding the result.
-// Every stage ends with a block barrier (callers must call it uniformly).
-template <bool INV>
+// Every stage ends with a block barrier (callers must call it uniformly), or a
+// wave-local one when WAVE (the transform is private to one wave).
+template <bool INV, bool WAVE = false>
 __device__ __forceinline__ float2* fft_pp(float2* a, float2* b, const float2* tw, const Fft1D& f, int c, int g,
                           int TPC, int ES, int CS, bool active) {
     int Ns = 1;
@@ -170,7 +176,8 @@ __device__ __forceinline__ float2* fft_pp(float2* a, float2* b, const float2* tw
                 default: stage_pp<7, INV>(src, dst, tw, f.L, Ns, c, g, TPC, ES, CS); break;
             }
         }
-        __syncthreads();
+        if constexpr (WAVE) wave_sync();
+        else __syncthreads();
         Ns *= R;
         float2* t = src;
         src = dst;
@@ -400,10 +407,13 @@ constexpr int kCThreads = 1024;
 // AXIS 1 = y (stride Hp), 2 = z (stride My*Hp).  ZMODE: 0 = one FFT (fwd/inv by INV),
 // 1 = fwd * K * inv.
 #include "fftconv_col.inc"
+#include "fft_reg.inc"
+#include "fftconv_2f.inc"
+#include "fftconv_x.inc"
 
 // ------------------------------------------------------------------ host side
 
-Fft1D make_fft(int L, DBuf<float2>& tw, hipStream_t s) {
+Fft1D make_fft(int L, bool allow_2f, DBuf<float2>& tw, hipStream_t s) {
     Fft1D f;
     f.L = L;
     int m = L;
@@ -419,6 +429,10 @@ Fft1D make_fft(int L, DBuf<float2>& tw, hipStream_t s) {
     while (m % 5 == 0) push(5);
     while (m % 7 == 0) push(7);
     SD_CHECK(m == 1, SPIMDECON_ERR_ARG, "FFT length " + std::to_string(L) + " is not 2,3,5,7-smooth");
+#define SD_2F_LOOKUP(A, B) \
+    if (L == (A) * (B)) { f.n1 = (A); f.n2 = (B); }
+    if (allow_2f) { SD_2F_SIZES(SD_2F_LOOKUP) }
+#undef SD_2F_LOOKUP
     std::vector<float2> h(L);
     for (int i = 0; i < L; ++i) {
         const double ang = -2.0 * M_PI * double(i) / double(L);
@@ -431,14 +445,17 @@ Fft1D make_fft(int L, DBuf<float2>& tw, hipStream_t s) {
     return f;
 }
 
-unsigned x_grid(const SpectralPlan& p) {
-    const int64_t npairs = (p.g.My * p.g.Mz + 1) / 2;
-    int64_t b = ceil_div(npairs, kXPairs);
-    return unsigned(std::min<int64_t>(b, 256 * 8));
-}
-
 size_t x_lds(const SpectralPlan& p) {
     return size_t(p.g.Mx + kXPairs * x_wave_elems(int(p.g.Mx))) * sizeof(float2);
+}
+
+// x-pass grid, shared by k_xpass and k_xrows (also the number of stats
+// partials an update pass writes)
+unsigned x_grid(const SpectralPlan& p) {
+    const int64_t nrows = p.g.My * p.g.Mz;
+    const int64_t npairs = (nrows + 1) / 2;
+    int64_t b = ceil_div(npairs, kXPairs);
+    return unsigned(std::min<int64_t>(b, 256 * 8));
 }
 
 XArgs base_args(const SpectralPlan& p) {
@@ -452,8 +469,42 @@ XArgs base_args(const SpectralPlan& p) {
     return a;
 }
 
+// k_xrows when the rows allow 16-B voxel access; false = use k_xpass
+template <int MODE>
+bool launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+    const int nx = int(p.g.nx);
+    const int U = int(ceil_div(p.Hp / 2, 64));
+    const int UV = int(ceil_div(nx / 4, 64));
+    const size_t va = st == Store::F32 ? 16 : 8;
+    auto al = [](const void* q, size_t n) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % n == 0; };
+    if (nx % 4 != 0 || U > 4 || (UV != U && UV != U - 1) || !al(a.img, va) || !al(a.w, va) ||
+        !al(a.psi_in, 16) || !al(a.psi_out, 16))
+        return false;
+    const size_t lds = x_lds(p);
+    SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
+    SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
+    const unsigned grid = x_grid(p);
+    const int sv = st == Store::F32 ? 0 : 1;
+#define SD_XR(SV, UU, VV)                                                                         \
+    if (sv == SV && U == UU && UV == VV) {                                                        \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xrows<MODE, SV, UU, VV>),    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));        \
+        hipLaunchKernelGGL((k_xrows<MODE, SV, UU, VV>), dim3(grid), dim3(kXThreads), lds, s, a); \
+    }
+#define SD_XR_S(SV) SD_XR(SV, 1, 1) SD_XR(SV, 2, 1) SD_XR(SV, 2, 2) SD_XR(SV, 3, 2) SD_XR(SV, 3, 3) \
+                    SD_XR(SV, 4, 3) SD_XR(SV, 4, 4)
+    SD_XR_S(0) SD_XR_S(1)
+#undef SD_XR_S
+#undef SD_XR
+    SD_HIP(hipGetLastError());
+    return true;
+}
+
 template <int MODE>
 void launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+    if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
+        if (launch_xrows<MODE>(a, st, p, s)) return;
+    }
     const size_t lds = x_lds(p);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
     SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
@@ -476,8 +527,35 @@ int col_tx(int L) {
     fail(SPIMDECON_ERR_ARG, "column FFT length " + std::to_string(L) + " exceeds the LDS tile");
 }
 
+template <int AXIS, int MODE>
+void launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+    const int L = f.L;
+    const size_t lds = size_t(L * k2fTX + L) * sizeof(float2);
+    SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "column LDS too large");
+    const int64_t ntiles = (p.Hp / k2fTX) * (AXIS == 1 ? p.g.Mz : p.g.My);
+    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * 2));
+    switch (f.n1 * 1000 + f.n2) {
+#define SD_2F_C(A, B)                                                                             \
+    case (A) * 1000 + (B):                                                                        \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE>),    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));        \
+        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE>), dim3(grid), dim3(k2fColThreads), lds, s, \
+                           p.g, p.Hp, f.tw, C, K);                                                \
+        break;
+        SD_2F_SIZES(SD_2F_C)
+#undef SD_2F_C
+        default: fail(SPIMDECON_ERR_ARG, "no two-factor column kernel for this length");
+    }
+    SD_HIP(hipGetLastError());
+}
+
 template <int AXIS, bool INV, int ZMODE>
 void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+    if (f.n1) {
+        launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s);
+        return;
+    }
     const int tx = col_tx(f.L);
     SD_CHECK(f.L * tx / 2 <= kColMaxU * kCThreads, SPIMDECON_ERR_ARG, "column tile exceeds prefetch registers");
     const size_t lds = size_t(2 * f.L * tx + f.L) * sizeof(float2);
@@ -500,25 +578,41 @@ void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* 
 
 }  // namespace
 
-int64_t engine_fast_size(int64_t need, bool even) {
-    for (int64_t m = std::max<int64_t>(need, 1);; ++m) {
+int64_t engine_fast_size(int64_t need, bool even, int policy) {
+    need = std::max<int64_t>(need, 1);
+    int64_t smooth = 0;
+    for (int64_t m = need;; ++m) {
         if (even && (m & 1)) continue;
         int64_t r = m;
         for (int64_t q : {2, 3, 5, 7})
             while (r % q == 0) r /= q;
-        if (r == 1) return m;
+        if (r == 1) {
+            smooth = m;
+            break;
+        }
     }
+    int64_t fast = 0;
+#define SD_2F_PICK(A, B) \
+    if ((A) * (B) >= need && (fast == 0 || (A) * (B) < fast)) fast = (A) * (B);
+    SD_2F_SIZES(SD_2F_PICK)
+#undef SD_2F_PICK
+    if (policy == 2 || fast == 0) {
+        SD_CHECK(policy != 1, SPIMDECON_ERR_ARG, "length " + std::to_string(need) + " beyond the fast-path table");
+        return smooth;
+    }
+    if (policy == 1) return fast;
+    return fast * 4 <= smooth * 5 ? fast : smooth;
 }
 
-void SpectralPlan::create(const SlabGeom& geom) {
+void SpectralPlan::create(const SlabGeom& geom, bool allow_2f) {
     g = geom;
     SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");
     Hx = g.Mx / 2 + 1;
     Hp = ceil_div(Hx, 16) * 16;  // column tiles of 16 (or 8/4) complex stay 128-B aligned
     hipStream_t s = nullptr;
-    fx = make_fft(int(g.Mx), twx, s);
-    fy = make_fft(int(g.My), twy, s);
-    fz = make_fft(int(g.Mz), twz, s);
+    fx = make_fft(int(g.Mx), allow_2f, twx, s);
+    fy = make_fft(int(g.My), allow_2f, twy, s);
+    fz = make_fft(int(g.Mz), allow_2f, twz, s);
     const int64_t nrows = g.My * g.Mz;
     std::vector<int> rm(nrows), ro(nrows);
     auto mir = [](int64_t sidx, int64_t n) -> int64_t {

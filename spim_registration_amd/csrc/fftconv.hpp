@@ -35,6 +35,7 @@ struct Fft1D {
     uint64_t radix_packed = 0;   // radix of stage s in bits [4s, 4s+4) (no indexed array:
                                  // a dynamically indexed kernel-argument array goes to scratch)
     const float2* tw = nullptr;  // device table exp(-2*pi*i*m/L), m < L
+    int n1 = 0, n2 = 0;          // two-factor fast path (L = n1 * n2), 0 = Stockham
     __host__ __device__ int radix(int s) const { return int((radix_packed >> (4 * s)) & 15u); }
 };
 
@@ -47,12 +48,15 @@ struct SpectralPlan {
     DBuf<int> row_mirror;  // [My*Mz] local source row (lz*ny+ly) of the mirror extension; -1 skip
     DBuf<int> row_one;     // [My*Mz] own local row if interior; -2 constant 1; -1 skip
     int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
-    void create(const SlabGeom& geom);
+    // allow_2f: use the two-factor register kernels for lengths in the fast-path table
+    void create(const SlabGeom& geom, bool allow_2f);
 };
 
-// smallest M >= need whose factors are all in {2,3,5,7} and that the engine
-// supports (even when `even`)
-int64_t engine_fast_size(int64_t need, bool even);
+// FFT length for `need` samples (even when `even`).  policy 0: the two-factor
+// fast-path size when it is within 25% of the smallest 2,3,5,7-smooth size,
+// else that smooth size (Stockham path); 1: always the fast-path table;
+// 2: always the smooth size.
+int64_t engine_fast_size(int64_t need, bool even, int policy = 0);
 
 // ---- passes (all asynchronous on `s`) ----
 // psi -> C (x-spectra of the mirror-extended psi rows)

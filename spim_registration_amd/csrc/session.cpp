@@ -157,9 +157,10 @@ void Session::build_spectra() {
             SD_CHECK(g.nz >= g.cz + 1, SPIMDECON_ERR_ARG,
                      "slab thinner than kernel half size + 1 (" + std::to_string(g.nz) + " < " +
                          std::to_string(g.cz + 1) + ")");
-        sl.pd.M[0] = engine_fast_size(g.nx + 2 * g.cx, true);
-        sl.pd.M[1] = engine_fast_size(g.ny + 2 * g.cy, false);
-        sl.pd.M[2] = engine_fast_size(g.nz + 2 * g.cz, false);
+        const int pol = backend_ == 1 ? 2 : p_.fft_pad_policy;
+        sl.pd.M[0] = engine_fast_size(g.nx + 2 * g.cx, true, pol);
+        sl.pd.M[1] = engine_fast_size(g.ny + 2 * g.cy, false, pol);
+        sl.pd.M[2] = engine_fast_size(g.nz + 2 * g.cz, false, pol);
         g.Mx = sl.pd.M[0];
         g.My = sl.pd.M[1];
         g.Mz = sl.pd.M[2];
@@ -193,7 +194,7 @@ void Session::build_spectra() {
                 }
             }
         } else {
-            sl.sp.create(g);
+            sl.sp.create(g, p_.fft_pad_policy != 2);
             const size_t ne = size_t(sl.sp.spectrum_elems());
             sl.C1.alloc(ne);
             sl.C2.alloc(ne);

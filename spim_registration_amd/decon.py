@@ -140,7 +140,7 @@ class Session:
 
     def __init__(self, dims_xyz, device=0, local_slabs=1, nranks=1, rank=0, comm_id=None,
                  nz_global=None, z_offset=0, storage_fp16=False, ij_threads=8, halo=None,
-                 fft_backend="engine"):
+                 fft_backend="engine", fft_pad_policy="auto"):
         self.lib = _lib.load()
         p = _lib.MvdParams()
         self.lib.mvd_params_default(C.byref(p))
@@ -157,6 +157,7 @@ class Session:
         p.storage_fp16 = int(bool(storage_fp16))
         p.ij_threads = int(ij_threads)
         p.fft_backend = {"engine": 0, "rocfft": 1}[fft_backend]
+        p.fft_pad_policy = {"auto": 0, "fast": 1, "smooth": 2}[fft_pad_policy]
         if halo is not None:
             for d in range(3):
                 p.halo[d] = int(halo[d])

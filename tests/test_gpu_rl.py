@@ -138,6 +138,29 @@ def test_engine_matches_rocfft_backend(gpu, shape, ksize):
     assert rel_l2(out[0][0], res.psi) < TOL
 
 
+@pytest.mark.parametrize("policy", ["fast", "smooth"])
+@pytest.mark.parametrize("shape,ksize", [((20, 24, 28), (7, 9, 11)), ((33, 17, 46), (5, 7, 3)),
+                                         ((30, 61, 40), (9, 5, 7)), ((12, 14, 500), (3, 3, 25)),
+                                         ((10, 500, 12), (3, 25, 3)), ((500, 10, 12), (25, 3, 3))])
+def test_engine_pad_policies(gpu, shape, ksize, policy):
+    """Two-factor register passes ("fast") and Stockham passes ("smooth") agree
+    with the rocFFT backend and the oracle."""
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
+    out = []
+    for be, pol in (("engine", policy), ("rocfft", "auto")):
+        with Session(shape[::-1], fft_backend=be, fft_pad_policy=pol) as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.OPTIMIZATION_II)
+            s.init_psi()
+            st = s.run(3, 0.0)
+            s.apply_mask()
+            out.append((s.get_psi(), st, s.fft_dims()))
+    assert rel_l2(out[0][0], out[1][0]) < 1e-5, out[0][2]
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_II, 3, 0.0)
+    assert rel_l2(out[0][0], res.psi) < TOL
+
+
 def test_initial_image_and_incremental_iterations(gpu):
     imgs, ws, ks, _ = small_case(V=2)
     init = imgs[0].copy()
