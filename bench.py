@@ -5,17 +5,19 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]): 4-view 512^3 synthetic PSF-blurred bead
-volume, 25^3 PSFs, multiview RL (PSFTYPE INDEPENDENT, lambda 0) -- one *step*
+Workload (BASELINE.json metric: "6-view 512^3 deconv"; configs[1] geometry and
+RL settings): 6-view 512^3 synthetic PSF-blurred bead volume, 25^3 PSFs,
+multiview RL (PSFTYPE INDEPENDENT, lambda 0) -- one *step*
 = one full RL iteration (all views, sequential per-view updates) over the
 volume, inputs resident in HBM.  With N ranks each GPU holds a 512^3 z-slab of
 a 512x512x(512N) volume (weak scaling); the slabs exchange 12-plane halos over
 RCCL before every convolution.  value = all ranks' voxels * steps / max-rank
 time / 1e6.
 
-Also reported: ``roofline`` of the RL pointwise update (quotient + update
-kernels, 28 B per voxel per view) timed with HIP events
-on the session's stream, and ``cpu_baseline`` = the oracle's float32 scipy.fft
+Also reported: ``roofline`` of the dominant engine pass (largest total time;
+algorithmic bytes per launch in DESIGN.md "Kernels") timed with HIP events on
+the session's stream, ``roofline_iteration`` (whole iteration against the
+engine's compulsory traffic), and ``cpu_baseline`` = the oracle's float32 scipy.fft
 restatement of the same iteration on a bounded sample (rank 0, N=1 only).
 """
 from __future__ import annotations
@@ -31,6 +33,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "Mvoxels/sec per RL iter, 6-view 512\u00b3 deconv; 1/2/4/8-GPU scaling"  # BASELINE.json
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -39,7 +42,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--views", type=int, default=4)
+    ap.add_argument("--views", type=int, default=6)
     ap.add_argument("--size", type=int, default=512, help="per-GPU cube edge")
     ap.add_argument("--ksize", type=int, default=25)
     ap.add_argument("--psftype", default="INDEPENDENT")
@@ -193,7 +196,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "Mvoxels/sec per RL iter, multiview deconv",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mvoxels/s per RL iteration",
             "n_gpus": world,

@@ -201,9 +201,14 @@ int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3);
 /* HIP stream the session launches on (hipStream_t as void*) */
 void* mvd_stream(mvd_session* h);
 /* per-kernel timing: when enabled, mvd_run records HIP events around every
- * kernel class; mvd_timing returns the accumulated ms per class:
- * [0] pad/update, [1] quotient, [2] r2c, [3] spectral multiply, [4] c2r,
- * [5] halo exchange, [6] launches counted for [0] (update kernel count) ... */
+ * kernel class; mvd_timing fills out16[0..7] with the accumulated ms and
+ * out16[8..15] with the launch count of each class:
+ *   engine backend: [0] x update pass, [1] x quotient pass, [2] y passes,
+ *                   [3] z convolve passes, [4] psi forward x pass,
+ *                   [5] halo exchange, [6] stats reduce
+ *   rocFFT backend: [0] update + pad, [1] quotient + pad, [2] R2C,
+ *                   [3] spectral multiply, [4] C2R, [5] halo exchange,
+ *                   [6] stats reduce */
 int mvd_enable_timing(mvd_session* h, int on);
 int mvd_timing(mvd_session* h, double* out16);
 
