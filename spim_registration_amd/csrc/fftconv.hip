@@ -527,35 +527,41 @@ int col_tx(int L) {
     fail(SPIMDECON_ERR_ARG, "column FFT length " + std::to_string(L) + " exceeds the LDS tile");
 }
 
+// two-factor column pass; false when the buffer-offset path does not apply
 template <int AXIS, int MODE>
-void launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
     const int L = f.L;
     const size_t lds = size_t(L * k2fTX + L) * sizeof(float2);
-    SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "column LDS too large");
+    const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
+    if (lds > 80 * 1024 || bytes >= (uint64_t(1) << 31)) return false;
     const int64_t ntiles = (p.Hp / k2fTX) * (AXIS == 1 ? p.g.Mz : p.g.My);
-    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * 2));
-    switch (f.n1 * 1000 + f.n2) {
-#define SD_2F_C(A, B)                                                                             \
-    case (A) * 1000 + (B):                                                                        \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE>),    \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));        \
-        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE>), dim3(grid), dim3(k2fColThreads), lds, s, \
-                           p.g, p.Hp, f.tw, C, K);                                                \
-        break;
-        SD_2F_SIZES(SD_2F_C)
-#undef SD_2F_C
-        default: fail(SPIMDECON_ERR_ARG, "no two-factor column kernel for this length");
+    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * 2 * 4));
+    // the fused z pass keeps the larger factor in phases A/C and multiplies by K
+    // on the smaller one (phase B), which bounds its registers
+    const int n1 = MODE == 2 ? std::min(f.n1, f.n2) : f.n1;
+    const int n2 = MODE == 2 ? std::max(f.n1, f.n2) : f.n2;
+    bool done = false;
+#define SD_2F_C1(A, B)                                                                                   \
+    if (!done && n1 == (A) && n2 == (B)) {                                                               \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE>),           \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));               \
+        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE>), dim3(grid), dim3(k2fColThreads), lds, s, p.g,   \
+                           p.Hp, f.tw, C, K, uint32_t(bytes));                                           \
+        done = true;                                                                                     \
     }
+#define SD_2F_C(A, B) \
+    if constexpr (MODE == 2) { SD_2F_C1((A < B ? A : B), (A < B ? B : A)) } else { SD_2F_C1(A, B) }
+    SD_2F_SIZES(SD_2F_C)
+#undef SD_2F_C
+#undef SD_2F_C1
+    SD_CHECK(done, SPIMDECON_ERR_ARG, "no two-factor column kernel for this length");
     SD_HIP(hipGetLastError());
+    return true;
 }
 
 template <int AXIS, bool INV, int ZMODE>
 void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
-    if (f.n1) {
-        launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s);
-        return;
-    }
+    if (f.n1 && launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s)) return;
     const int tx = col_tx(f.L);
     SD_CHECK(f.L * tx / 2 <= kColMaxU * kCThreads, SPIMDECON_ERR_ARG, "column tile exceeds prefetch registers");
     const size_t lds = size_t(2 * f.L * tx + f.L) * sizeof(float2);
