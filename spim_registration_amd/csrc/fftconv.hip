@@ -9,6 +9,7 @@
 #include "fftconv.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace spimdecon {
 
@@ -207,6 +208,8 @@ struct XArgs {
     const float* kern;
     int kx, ky, kz;
     float kscale;
+    uint32_t spec_bytes;  // k_xrows buffer ranges (< 2 GiB each)
+    uint32_t nvox;
 };
 
 constexpr int kXThreads = 256;             // four waves; one packed row pair per wave
@@ -410,6 +413,7 @@ constexpr int kCThreads = 1024;
 #include "fft_reg.inc"
 #include "fftconv_2f.inc"
 #include "fftconv_x.inc"
+#include "fftconv_xt.inc"
 
 // ------------------------------------------------------------------ host side
 
@@ -469,41 +473,97 @@ XArgs base_args(const SpectralPlan& p) {
     return a;
 }
 
-// k_xrows when the rows allow 16-B voxel access; false = use k_xpass
+// two-factor x tiles: lengths >= 256 of the fast-path table
+#define SD_X2F_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24) M(20, 32) M(25, 32)
+
+bool aligned_to(const void* q, size_t n) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % n == 0; }
+
+// buffer ranges for k_xrows / k_xtile; false when a buffer exceeds the 31-bit range
+bool x_buffer_args(const XArgs& a, Store st, const SpectralPlan& p, XArgs& b) {
+    const size_t va = st == Store::F32 ? 16 : 8;
+    const uint64_t spec_bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
+    const uint64_t nvox = uint64_t(p.g.nx) * p.g.ny * p.g.nz;
+    if (p.g.nx % 4 != 0 || !aligned_to(a.img, va) || !aligned_to(a.w, va) || !aligned_to(a.psi_in, 16) ||
+        !aligned_to(a.psi_out, 16) || spec_bytes >= kOOB || nvox * 4 >= kOOB)
+        return false;
+    b = a;
+    b.spec_bytes = uint32_t(spec_bytes);
+    b.nvox = uint32_t(nvox);
+    return true;
+}
+
+// k_xtile for two-factor lengths; returns the grid, 0 when it does not apply
 template <int MODE>
-bool launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+    static const bool on = [] {  // SPIMDECON_X2F=0: per-wave Stockham rows (A/B measurements)
+        const char* e = std::getenv("SPIMDECON_X2F");
+        return !(e && e[0] == '0');
+    }();
+    XArgs b;
+    if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
+    const int L = int(p.g.Mx);
+    const size_t lds = size_t(L + 1 + kXtPairs * (L + 1)) * sizeof(float2);
+    if (lds > 160 * 1024) return 0;
+    const int64_t npairs = (p.g.My * p.g.Mz + 1) / 2;
+    const int64_t ntiles = ceil_div(npairs, kXtPairs);
+    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+    const unsigned grid = unsigned(std::min<int64_t>({ntiles, 256 * per_cu, 4096}));
+    const int sv = st == Store::F32 ? 0 : 1;
+    bool done = false;
+#define SD_XT(SV, A, B)                                                                               \
+    if (!done && sv == SV && L == (A) * (B)) {                                                       \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B>),         \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));           \
+        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B>), dim3(grid), dim3(kXtThreads), lds, s, b);     \
+        done = true;                                                                                 \
+    }
+#define SD_XT_S(A, B) SD_XT(0, A, B) SD_XT(1, A, B)
+    SD_X2F_SIZES(SD_XT_S)
+#undef SD_XT_S
+#undef SD_XT
+    if (!done) return 0;
+    SD_HIP(hipGetLastError());
+    return grid;
+}
+
+// k_xrows when the rows allow 16-B voxel access; returns the grid, 0 = use k_xpass
+template <int MODE>
+unsigned launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
     const int nx = int(p.g.nx);
     const int U = int(ceil_div(p.Hp / 2, 64));
     const int UV = int(ceil_div(nx / 4, 64));
-    const size_t va = st == Store::F32 ? 16 : 8;
-    auto al = [](const void* q, size_t n) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % n == 0; };
-    if (nx % 4 != 0 || U > 4 || (UV != U && UV != U - 1) || !al(a.img, va) || !al(a.w, va) ||
-        !al(a.psi_in, 16) || !al(a.psi_out, 16))
-        return false;
-    const size_t lds = x_lds(p);
+    XArgs b;
+    if (U > 4 || (UV != U && UV != U - 1) || !x_buffer_args(a, st, p, b)) return 0;
+    const int Mx = int(p.g.Mx);
+    const size_t lds = size_t(Mx + kXPairs * xrows_wave_elems(Mx, false)) * sizeof(float2);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
     SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
     const unsigned grid = x_grid(p);
     const int sv = st == Store::F32 ? 0 : 1;
-#define SD_XR(SV, UU, VV)                                                                         \
-    if (sv == SV && U == UU && UV == VV) {                                                        \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xrows<MODE, SV, UU, VV>),    \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));        \
-        hipLaunchKernelGGL((k_xrows<MODE, SV, UU, VV>), dim3(grid), dim3(kXThreads), lds, s, a); \
+    bool done = false;
+#define SD_XR(SV, UU, VV)                                                                               \
+    if (!done && sv == SV && U == UU && UV == VV) {                                                     \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xrows<MODE, SV, UU, VV, 0, 0>),    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));              \
+        hipLaunchKernelGGL((k_xrows<MODE, SV, UU, VV, 0, 0>), dim3(grid), dim3(kXThreads), lds, s, b); \
+        done = true;                                                                                    \
     }
-#define SD_XR_S(SV) SD_XR(SV, 1, 1) SD_XR(SV, 2, 1) SD_XR(SV, 2, 2) SD_XR(SV, 3, 2) SD_XR(SV, 3, 3) \
-                    SD_XR(SV, 4, 3) SD_XR(SV, 4, 4)
+#define SD_XR_S(SV) SD_XR(SV, 1, 1) SD_XR(SV, 2, 1) SD_XR(SV, 2, 2) SD_XR(SV, 3, 2) \
+                    SD_XR(SV, 3, 3) SD_XR(SV, 4, 3) SD_XR(SV, 4, 4)
     SD_XR_S(0) SD_XR_S(1)
 #undef SD_XR_S
 #undef SD_XR
+    SD_CHECK(done, SPIMDECON_ERR_ARG, "no x-row kernel for this configuration");
     SD_HIP(hipGetLastError());
-    return true;
+    return grid;
 }
 
+// launches the x pass; returns its grid (= number of stats partials of an update pass)
 template <int MODE>
-void launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
+unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
     if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
-        if (launch_xrows<MODE>(a, st, p, s)) return;
+        if (const unsigned gt = launch_xtile<MODE>(a, st, p, s)) return gt;
+        if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) return gr;
     }
     const size_t lds = x_lds(p);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
@@ -519,6 +579,7 @@ void launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
         hipLaunchKernelGGL((k_xpass<MODE, 1>), dim3(grid), dim3(kXThreads), lds, s, a);
     }
     SD_HIP(hipGetLastError());
+    return grid;
 }
 
 int col_tx(int L) {
@@ -712,8 +773,7 @@ int64_t engine_update(const SpectralPlan& p, Store st, const float2* Cin, const 
     a.w = w;
     a.lambda = lambda;
     a.partials = partials;
-    launch_x<XM_UPDATE>(a, st, p, s);
-    return x_grid(p);
+    return launch_x<XM_UPDATE>(a, st, p, s);
 }
 
 }  // namespace spimdecon

@@ -34,7 +34,7 @@ def main(out):
                 seen.add(key)
                 dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     avg = lambda xs: sum(xs) / len(xs) if xs else float("nan")
-    cols = ["SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+    cols = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
             "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS",
             "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"]
     print("| kernel | us (avg) | HBM MB/launch (2*FETCH+WRITE) | GB/s | " + " | ".join(cols) + " |")
