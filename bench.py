@@ -56,6 +56,30 @@ def parse():
     return ap.parse_args()
 
 
+# engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
+PMC_KERNELS = {"z_convolve": ("k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
+               "x_update": ("k_xtile<2,", "k_xrows<2,", "k_xpass<2,"),
+               "x_quotient": ("k_xtile<1,", "k_xrows<1,", "k_xpass<1,")}
+
+
+def pmc_traffic(cls, M, args):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (profiles/pmc_traffic.json, same FFT dims and storage), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if args.backend != "engine" or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    if list(d.get("fft_dims", [])) != list(M) or bool(d.get("fp16", False)) != bool(args.fp16):
+        return None, None
+    for name, ent in d["kernels"].items():
+        if name.startswith(PMC_KERNELS.get(cls, ())):
+            if cls == "z_convolve" and not name.rstrip(">").endswith("2"):
+                continue   # the fused z pass is MODE 2
+            return int(ent["hbm_bytes_per_launch"]), f"{d['file']}: {name}"
+    return None, None
+
+
 def cpu_baseline(args):
     """The oracle (numpy + scipy.fft float32, multithreaded) on a bounded sample:
     V views of cpu_size^3 with the same PSFs; 1 warm-up + 2 timed iterations."""
@@ -181,10 +205,13 @@ def main():
         if best is not None:
             nm, _, byts, avg = best
             achieved = byts / (avg * 1e-3) / 1e9
+            traffic, tsrc = pmc_traffic(nm, M, args)
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": nm, "algorithmic_bytes_per_launch": int(byts),
                         "avg_launch_ms": round(avg, 5)}
+            if tsrc:
+                roofline["traffic_source"] = tsrc
         t_iter = ms_per_step * 1e-3
         it_roof = {"achieved": round(b_iter / t_iter / 1e9, 1), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(b_iter / t_iter / 1e9 / HBM_PEAK_GBS, 4),

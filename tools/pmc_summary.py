@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 --pmc passes of tools/pmc_engine.sh per kernel.
 
-usage: python tools/pmc_summary.py OUTDIR  (OUTDIR holds p1/ .. p4/)
+usage: python tools/pmc_summary.py OUTDIR [--json OUT.json --dims MX,MY,MZ [--fp16]]
+(OUTDIR holds p1/ .. p4/; the JSON feeds bench.py's roofline.traffic)
 
 Per kernel (averaged over its dispatches): duration, HBM traffic per launch
 (FETCH_SIZE x 2 + WRITE_SIZE, in KB units per rocprofv3; FETCH_SIZE counts
@@ -21,7 +22,7 @@ def short(name):
     return m.group(1) if m else name[:60]
 
 
-def main(out):
+def main(out, json_out=None, dims=None, fp16=False):
     vals = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(out, "p*", "*_counter_collection.csv"))):
@@ -39,6 +40,7 @@ def main(out):
             "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"]
     print("| kernel | us (avg) | HBM MB/launch (2*FETCH+WRITE) | GB/s | " + " | ".join(cols) + " |")
     print("|---|" + "---|" * (3 + len(cols)))
+    table = {}
     for k in sorted(vals):
         v = vals[k]
         fetch = avg(v.get("FETCH_SIZE", []))
@@ -48,7 +50,25 @@ def main(out):
         row = [k, f"{t * 1e6:.1f}", f"{traffic / 1e6:.1f}", f"{traffic / t / 1e9:.0f}"]
         row += [f"{avg(v.get(c, [])):.3g}" for c in cols]
         print("| " + " | ".join(row) + " |")
+        table[k] = {"avg_us": round(t * 1e6, 2), "hbm_bytes_per_launch": int(traffic),
+                    "fetch_kb_x2": 2 * fetch, "write_kb": write}
+    if json_out:
+        import json
+        with open(json_out, "w") as f:
+            json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                 "tools/pmc_engine.sh; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
+                                 "(gfx950 FETCH_SIZE counts half of wide reads)",
+                       "file": os.path.relpath(json_out, os.path.dirname(os.path.dirname(
+                           os.path.abspath(__file__)))),
+                       "fft_dims": dims, "fp16": fp16, "kernels": table}, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("outdir")
+    ap.add_argument("--json")
+    ap.add_argument("--dims", default="540,540,540")
+    ap.add_argument("--fp16", action="store_true")
+    a = ap.parse_args()
+    main(a.outdir, a.json, [int(x) for x in a.dims.split(",")], a.fp16)
