@@ -234,13 +234,31 @@ typedef struct spim_peak {
     int32_t is_min, is_max;
 } spim_peak;
 
+/* InterestPoint(Value) of spim.fiji.spimdata.interestpoints (id = index) */
+typedef struct spim_interest_point {
+    double  pos[3];          /* x, y, z (sub-pixel with localization 1)             */
+    float   intensity;       /* |dog| (localization 0) or the fitted value (1)       */
+    int32_t is_max;
+} spim_interest_point;
+
 void spim_dog_params_default(spim_dog_params* p);
 
 /* img: dims {nx, ny, nz} x-fastest (not modified).  dog_out (optional, may be
  * NULL) receives the DoG image.  peaks: capacity max_peaks, *npeaks = total
- * found (may exceed max_peaks: then only max_peaks were written). */
+ * found (may exceed max_peaks: then only max_peaks were written).  These are
+ * the DoG extrema with |v| >= threshold (localization 0) or threshold / 10
+ * (localization 1), i.e. DifferenceOfGaussianNewPeakFinder.getSimplePeaks. */
 int spim_dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p,
                      float* dog_out, spim_peak* peaks, int64_t max_peaks, int64_t* npeaks);
+
+/* ProcessDOG.compute's result (ProcessDOG.java:150-168): the peaks above
+ * after Localization -- localization 0: Localization.noLocalization
+ * (Localization.java:19-45); 1: quadratic sub-pixel fit, kept when
+ * |fitted value| > threshold (Localization.java:47-88).  Same capacity rule
+ * as spim_dog_compute. */
+int spim_dog_interest_points(const float* img, const int64_t* dims, const spim_dog_params* p,
+                             float* dog_out, spim_interest_point* out, int64_t max_out,
+                             int64_t* nout);
 
 #ifdef __cplusplus
 }

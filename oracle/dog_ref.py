@@ -7,6 +7,11 @@ SeparableConvolutionCUDALib are not in the container; their published
 algorithms are restated below.  Paths relative to
 ``/root/reference/src/main/java/``; IPD = spim/process/interestpointdetection/.
 
+The sub-pixel quadratic fit (imglib1 ``SubpixelLocalization``, external) is
+restated after the reference's own fit in LaPlaceFunctions.java (same author,
+same finite differences); its tolerance rule is an assumption (see
+``quadratic_localization``).
+
 The restated variant is the GPU "accurate" path: blocks copied with
 ``extendMirrorSingle`` (IPD/DifferenceOfGaussianCUDA.java:153-154,170), float
 kernels zero-padded to the supported size
@@ -223,13 +228,111 @@ def find_peaks(dog: np.ndarray, min_value: float, ij_threads: int = 8):
     return [peaks[i] for i in order]
 
 
+MAX_NUM_MOVES = 10        # IPD/Localization.java:57 (spl.setMaxNumMoves(10))
+MAXIMA_TOLERANCE = 0.01   # imglib1 SubpixelLocalization default, allowMaximaTolerance = true (:56)
+
+
+def _hessian_and_gradient(d: np.ndarray, x: int, y: int, z: int):
+    """Finite differences of the quadratic fit, in the reference's arithmetic
+    (mpicbg/spim/registration/bead/laplace/LaPlaceFunctions.java:288-466):
+    diagonal = float(v(+1) - 2 v(0)) + v(-1) in double; cross terms
+    ((a - b) / 2 - (c - d) / 2) / 2 in float; gradient (v(+1) - v(-1)) / 2 in double."""
+    v = lambda dx, dy, dz: d[z + dz, y + dy, x + dx]   # float32 scalars
+    two = np.float32(2)
+    temp = two * v(0, 0, 0)
+    H = np.zeros(9)
+    H[0] = float(v(1, 0, 0) - temp) + float(v(-1, 0, 0))
+    H[4] = float(v(0, 1, 0) - temp) + float(v(0, -1, 0))
+    H[8] = float(v(0, 0, 1) - temp) + float(v(0, 0, -1))
+
+    def cross(a, b, c, e):
+        return float(((a - b) / two - (c - e) / two) / two)
+    H[5] = H[7] = cross(v(0, 1, 1), v(0, -1, 1), v(0, 1, -1), v(0, -1, -1))
+    H[2] = H[6] = cross(v(1, 0, 1), v(-1, 0, 1), v(1, 0, -1), v(-1, 0, -1))
+    H[1] = H[3] = cross(v(1, 1, 0), v(-1, 1, 0), v(1, -1, 0), v(-1, -1, 0))
+    g = np.array([(float(v(1, 0, 0)) - float(v(-1, 0, 0))) / 2.0,
+                  (float(v(0, 1, 0)) - float(v(0, -1, 0))) / 2.0,
+                  (float(v(0, 0, 1)) - float(v(0, 0, -1))) / 2.0])
+    return H, g
+
+
+def _invert3(a):
+    """LaPlaceFunctions.java:243-286 (det, adjugate / det); None when det == 0."""
+    det = (a[0] * a[4] * a[8] + a[3] * a[7] * a[2] + a[6] * a[1] * a[5]
+           - a[2] * a[4] * a[6] - a[5] * a[7] * a[0] - a[8] * a[1] * a[3])
+    if det == 0:
+        return None
+    return np.array([(a[4] * a[8] - a[5] * a[7]) / det, (a[2] * a[7] - a[1] * a[8]) / det,
+                     (a[1] * a[5] - a[2] * a[4]) / det, (a[5] * a[6] - a[3] * a[8]) / det,
+                     (a[0] * a[8] - a[2] * a[6]) / det, (a[2] * a[3] - a[0] * a[5]) / det,
+                     (a[3] * a[7] - a[4] * a[6]) / det, (a[1] * a[6] - a[0] * a[7]) / det,
+                     (a[0] * a[4] - a[1] * a[3]) / det])
+
+
+def quadratic_localization(dog: np.ndarray, peaks, max_moves: int = MAX_NUM_MOVES,
+                           tolerance: float = MAXIMA_TOLERANCE):
+    """Sub-pixel quadratic fit of each peak (IPD/Localization.java:47-88 via
+    imglib1 ``SubpixelLocalization``; the iteration restated after the
+    reference's own fit, LaPlaceFunctions.java:30-170).
+
+    Per peak: Hessian H and gradient g at the current voxel, offset
+    X = -H^-1 g; every axis with |X_d| > 0.5 + moves * tolerance moves one voxel
+    towards sign(X_d); repeat up to ``max_moves`` moves.  A move onto the image
+    border, a singular H or no stable solution leave the peak as detected
+    (integer position, value = |v|).  Otherwise position = voxel + (float) X,
+    value = (float) v(voxel) + (float) (X . g / 2).
+    Returns [(x, y, z, value)] as float32 (value is signed)."""
+    d = np.asarray(dog, np.float32)
+    nz, ny, nx = d.shape
+    dims = (nx, ny, nz)
+    out = []
+    for pk in peaks:
+        x0, y0, z0, inten = pk[0], pk[1], pk[2], pk[3]
+        p = [int(x0), int(y0), int(z0)]
+        res = (np.float32(x0), np.float32(y0), np.float32(z0), np.float32(inten))
+        moves = 0
+        stable = False
+        valid = True
+        X = g = None
+        while True:
+            moves += 1
+            H, g = _hessian_and_gradient(d, *p)
+            A = _invert3(H)
+            if A is None:
+                valid = False
+                break
+            X = -np.array([A[0] * g[0] + A[1] * g[1] + A[2] * g[2],
+                           A[3] * g[0] + A[4] * g[1] + A[5] * g[2],
+                           A[6] * g[0] + A[7] * g[1] + A[8] * g[2]])
+            stable = True
+            thr = 0.5 + moves * tolerance
+            for a in range(3):
+                if abs(X[a]) > thr:
+                    p[a] += 1 if X[a] > 0 else -1
+                    stable = False
+            if not stable and any(p[a] <= 0 or p[a] >= dims[a] - 1 for a in range(3)):
+                valid = False
+                break
+            if stable or moves > max_moves:
+                break
+        if valid and stable:
+            fit = (X[0] * g[0] + X[1] * g[1] + X[2] * g[2]) / 2.0
+            val = np.float32(d[p[2], p[1], p[0]]) + np.float32(fit)
+            res = (np.float32(p[0]) + np.float32(X[0]), np.float32(p[1]) + np.float32(X[1]),
+                   np.float32(p[2]) + np.float32(X[2]), np.float32(val))
+        out.append(res)
+    return out
+
+
 def process_dog(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008,
                 localization: int = 0, image_sigma=(0.5, 0.5, 0.5),
                 find_min: bool = False, find_max: bool = True,
                 min_intensity=float("nan"), max_intensity=float("nan"),
                 ij_threads: int = 8):
-    """IPD/ProcessDOG.java:40-178 with localization 0 (IPD/Localization.java:19-45).
-    Returns (peaks [(x,y,z,intensity)], dog image)."""
+    """IPD/ProcessDOG.java:40-178 with localization 0 (IPD/Localization.java:19-45)
+    or 1 (quadratic fit, :47-88).  Returns (points [(x, y, z, intensity)], dog
+    image); localization 1 keeps the points with |fitted value| > threshold and
+    reports the fitted value."""
     min_peak = f32(threshold) if localization == 0 else f32(f32(threshold) / f32(10.0))
     if (math.isnan(min_intensity) or math.isnan(max_intensity) or math.isinf(min_intensity)
             or math.isinf(max_intensity) or min_intensity == max_intensity):
@@ -240,4 +343,8 @@ def process_dog(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008,
     dog = dog_image(norm, sigma, image_sigma)
     peaks = find_peaks(dog, float(min_peak), ij_threads)
     out = [(p[0], p[1], p[2], p[3]) for p in peaks if (p[5] and find_max) or (p[4] and find_min)]
+    if localization == 1:
+        fitted = quadratic_localization(dog, out)
+        out = [(float(x), float(y), float(z), float(v)) for x, y, z, v in fitted
+               if abs(v) > np.float32(threshold)]
     return out, dog

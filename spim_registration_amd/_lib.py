@@ -62,6 +62,10 @@ class Peak(C.Structure):
                 ("intensity", C.c_float), ("is_min", C.c_int32), ("is_max", C.c_int32)]
 
 
+class InterestPointC(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("intensity", C.c_float), ("is_max", C.c_int32)]
+
+
 # name -> (restype, argtypes); exactly the declarations of include/spimdecon.h
 SIGNATURES = {
     "spimdecon_last_error": (C.c_char_p, []),
@@ -101,6 +105,8 @@ SIGNATURES = {
     "spim_dog_params_default": (None, [C.POINTER(DogParams)]),
     "spim_dog_compute": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf, C.POINTER(Peak),
                                    _i64, _pi64]),
+    "spim_dog_interest_points": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf,
+                                           C.POINTER(InterestPointC), _i64, _pi64]),
 }
 for _n in (15, 31, 63, 127):
     SIGNATURES[f"convolve_{_n}"] = SIGNATURES["convolve_7"]

@@ -376,19 +376,103 @@ void separable_convolve(float* image, const float* kx, const float* ky, const fl
 }
 
 // ---------------------------------------------------------------- DoG
-void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
-                 spim_peak* peaks, int64_t max_peaks, int64_t* npeaks) {
-    SD_CHECK(img && dims && p && npeaks, SPIMDECON_ERR_ARG, "null argument");
+// ---------------------------------------------------------------- quadratic localization
+// IPD/Localization.java:47-88 (imglib1 SubpixelLocalization, maxNumMoves 10,
+// allowMaximaTolerance); finite differences and 3x3 inverse as in the reference's
+// own fit, mpicbg/spim/registration/bead/laplace/LaPlaceFunctions.java:30-170,243-466.
+// One thread per peak; all fit arithmetic in double, -ffp-contract=off.
+struct LocOut {
+    float pos[3];
+    float value;
+};
+
+constexpr int kLocMaxMoves = 10;
+constexpr double kLocTolerance = 0.01;
+
+__global__ void k_localize(const float* __restrict__ dog, Dims3 d, const PeakOut* __restrict__ pk,
+                           int64_t np, LocOut* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const PeakOut q = pk[i];
+    int p[3] = {q.x, q.y, q.z};
+    const int64_t dim[3] = {d.nx, d.ny, d.nz};
+    auto v = [&](int dx, int dy, int dz) -> float {
+        return dog[(int64_t(p[2] + dz) * d.ny + (p[1] + dy)) * d.nx + (p[0] + dx)];
+    };
+    double X[3] = {0, 0, 0}, g[3] = {0, 0, 0};
+    bool stable = false, valid = true;
+    int moves = 0;
+    for (;;) {
+        ++moves;
+        const float temp = 2.0f * v(0, 0, 0);
+        double H[9];
+        H[0] = double(v(1, 0, 0) - temp) + double(v(-1, 0, 0));
+        H[4] = double(v(0, 1, 0) - temp) + double(v(0, -1, 0));
+        H[8] = double(v(0, 0, 1) - temp) + double(v(0, 0, -1));
+        auto cross = [](float a, float b, float c, float e) {
+            return double(((a - b) / 2.0f - (c - e) / 2.0f) / 2.0f);
+        };
+        H[5] = H[7] = cross(v(0, 1, 1), v(0, -1, 1), v(0, 1, -1), v(0, -1, -1));
+        H[2] = H[6] = cross(v(1, 0, 1), v(-1, 0, 1), v(1, 0, -1), v(-1, 0, -1));
+        H[1] = H[3] = cross(v(1, 1, 0), v(-1, 1, 0), v(1, -1, 0), v(-1, -1, 0));
+        g[0] = (double(v(1, 0, 0)) - double(v(-1, 0, 0))) / 2.0;
+        g[1] = (double(v(0, 1, 0)) - double(v(0, -1, 0))) / 2.0;
+        g[2] = (double(v(0, 0, 1)) - double(v(0, 0, -1))) / 2.0;
+        const double det = H[0] * H[4] * H[8] + H[3] * H[7] * H[2] + H[6] * H[1] * H[5] -
+                            H[2] * H[4] * H[6] - H[5] * H[7] * H[0] - H[8] * H[1] * H[3];
+        if (det == 0.0) {
+            valid = false;
+            break;
+        }
+        const double A[9] = {(H[4] * H[8] - H[5] * H[7]) / det, (H[2] * H[7] - H[1] * H[8]) / det,
+                             (H[1] * H[5] - H[2] * H[4]) / det, (H[5] * H[6] - H[3] * H[8]) / det,
+                             (H[0] * H[8] - H[2] * H[6]) / det, (H[2] * H[3] - H[0] * H[5]) / det,
+                             (H[3] * H[7] - H[4] * H[6]) / det, (H[1] * H[6] - H[0] * H[7]) / det,
+                             (H[0] * H[4] - H[1] * H[3]) / det};
+        for (int r = 0; r < 3; ++r) X[r] = -(A[3 * r] * g[0] + A[3 * r + 1] * g[1] + A[3 * r + 2] * g[2]);
+        stable = true;
+        const double thr = 0.5 + moves * kLocTolerance;
+        for (int a = 0; a < 3; ++a)
+            if (fabs(X[a]) > thr) {
+                p[a] += X[a] > 0 ? 1 : -1;
+                stable = false;
+            }
+        if (!stable)
+            for (int a = 0; a < 3; ++a)
+                if (p[a] <= 0 || p[a] >= dim[a] - 1) valid = false;
+        if (!valid || stable || moves > kLocMaxMoves) break;
+    }
+    LocOut o;
+    if (valid && stable) {
+        const double fit = (X[0] * g[0] + X[1] * g[1] + X[2] * g[2]) / 2.0;
+        for (int a = 0; a < 3; ++a) o.pos[a] = float(p[a]) + float(X[a]);
+        o.value = v(0, 0, 0) + float(fit);
+    } else {  // no stable fit: the peak stays as detected
+        o.pos[0] = float(q.x);
+        o.pos[1] = float(q.y);
+        o.pos[2] = float(q.z);
+        o.value = q.intensity;
+    }
+    out[i] = o;
+}
+
+// the DoG image (kept on the device) and the reference-ordered peak list
+struct DogRun {
+    Dims3 d{};
+    DBuf<float> dog;
+    std::vector<PeakOut> peaks;
+};
+
+void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
+             hipStream_t s, DogRun& r) {
+    SD_CHECK(img && dims && p, SPIMDECON_ERR_ARG, "null argument");
     SD_CHECK(dims[0] >= 1 && dims[1] >= 1 && dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
-    SD_CHECK(p->localization == 0, SPIMDECON_ERR_ARG,
-             "only localization 0 (none) is implemented; quadratic localization is SURVEY 8f next #4");
+    SD_CHECK(p->localization == 0 || p->localization == 1, SPIMDECON_ERR_ARG,
+             "localization must be 0 (none) or 1 (quadratic); the Gaussian fit is not implemented in "
+             "the reference either (Localization.java:90-96)");
     SD_CHECK(p->ij_threads >= 1, SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
-    check_device(p->device);
-    DeviceGuard guard(p->device);
-    hipStream_t s;
-    SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    struct SG { hipStream_t s; ~SG() { (void)hipStreamDestroy(s); } } sg{s};
     const Dims3 d{dims[0], dims[1], dims[2]};
+    r.d = d;
     const int64_t n = d.nx * d.ny * d.nz;
 
     // ProcessDOG.java:61-105
@@ -460,25 +544,89 @@ void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p
     hipLaunchKernelGGL(k_peaks_write, dim3(unsigned(nb)), dim3(kBlock), 0, s, dog, d, min_peak, wmin,
                        wmax, offsets.p, dpk.p, total);
     SD_HIP(hipGetLastError());
-    std::vector<PeakOut> hp(total);
-    if (total) SD_HIP(hipMemcpyAsync(hp.data(), dpk.p, total * sizeof(PeakOut), hipMemcpyDeviceToHost, s));
+    r.peaks.resize(total);
+    if (total)
+        SD_HIP(hipMemcpyAsync(r.peaks.data(), dpk.p, total * sizeof(PeakOut), hipMemcpyDeviceToHost, s));
     SD_HIP(hipStreamSynchronize(s));
     // reference order: per-thread lists by x % T, each in flat order (InteractiveIntegral.java:394,437-438)
     const int T = p->ij_threads;
-    std::stable_sort(hp.begin(), hp.end(),
+    std::stable_sort(r.peaks.begin(), r.peaks.end(),
                      [T](const PeakOut& a, const PeakOut& b) { return (a.x % T) < (b.x % T); });
+    r.dog = std::move(b1);
+}
+
+struct StreamHolder {
+    hipStream_t s = nullptr;
+    StreamHolder() { SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+    ~StreamHolder() { (void)hipStreamDestroy(s); }
+};
+
+// DifferenceOfGaussianNewPeakFinder.getSimplePeaks level: candidates with
+// |v| >= threshold (localization 0) or threshold / 10 (localization 1)
+void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
+                 spim_peak* peaks, int64_t max_peaks, int64_t* npeaks) {
+    SD_CHECK(npeaks && p, SPIMDECON_ERR_ARG, "null argument");
+    check_device(p->device);
+    DeviceGuard guard(p->device);
+    StreamHolder sh;
+    DogRun r;
+    dog_run(img, dims, p, dog_out, sh.s, r);
+    const int64_t total = int64_t(r.peaks.size());
     *npeaks = total;
     if (peaks) {
         const int64_t m = std::min(total, max_peaks);
         for (int64_t i = 0; i < m; ++i) {
-            peaks[i].x = hp[i].x;
-            peaks[i].y = hp[i].y;
-            peaks[i].z = hp[i].z;
-            peaks[i].intensity = hp[i].intensity;
-            peaks[i].is_min = hp[i].is_min;
-            peaks[i].is_max = hp[i].is_max;
+            peaks[i].x = r.peaks[i].x;
+            peaks[i].y = r.peaks[i].y;
+            peaks[i].z = r.peaks[i].z;
+            peaks[i].intensity = r.peaks[i].intensity;
+            peaks[i].is_min = r.peaks[i].is_min;
+            peaks[i].is_max = r.peaks[i].is_max;
         }
     }
+}
+
+// ProcessDOG.compute's result: interest points after Localization (:150-168)
+void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
+                         spim_interest_point* out, int64_t max_out, int64_t* nout) {
+    SD_CHECK(nout && p, SPIMDECON_ERR_ARG, "null argument");
+    check_device(p->device);
+    DeviceGuard guard(p->device);
+    StreamHolder sh;
+    DogRun r;
+    dog_run(img, dims, p, dog_out, sh.s, r);
+    std::vector<spim_interest_point> pts;
+    const int64_t np = int64_t(r.peaks.size());
+    if (p->localization == 0) {  // Localization.noLocalization (:19-45)
+        pts.resize(np);
+        for (int64_t i = 0; i < np; ++i) {
+            pts[i].pos[0] = r.peaks[i].x;
+            pts[i].pos[1] = r.peaks[i].y;
+            pts[i].pos[2] = r.peaks[i].z;
+            pts[i].intensity = r.peaks[i].intensity;
+            pts[i].is_max = r.peaks[i].is_max;
+        }
+    } else if (np > 0) {  // Localization.computeQuadraticLocalization (:47-88)
+        DBuf<PeakOut> dpk(np);
+        DBuf<LocOut> dloc(np);
+        SD_HIP(hipMemcpyAsync(dpk.p, r.peaks.data(), np * sizeof(PeakOut), hipMemcpyHostToDevice, sh.s));
+        hipLaunchKernelGGL(k_localize, dim3(unsigned(ceil_div(np, 256))), dim3(256), 0, sh.s, r.dog.p, r.d,
+                           dpk.p, np, dloc.p);
+        SD_HIP(hipGetLastError());
+        std::vector<LocOut> loc(np);
+        SD_HIP(hipMemcpyAsync(loc.data(), dloc.p, np * sizeof(LocOut), hipMemcpyDeviceToHost, sh.s));
+        SD_HIP(hipStreamSynchronize(sh.s));
+        for (int64_t i = 0; i < np; ++i) {
+            if (!(std::fabs(loc[i].value) > p->threshold)) continue;
+            spim_interest_point ip{};
+            for (int a = 0; a < 3; ++a) ip.pos[a] = loc[i].pos[a];
+            ip.intensity = loc[i].value;
+            ip.is_max = r.peaks[i].is_max;
+            pts.push_back(ip);
+        }
+    }
+    *nout = int64_t(pts.size());
+    if (out) std::copy(pts.begin(), pts.begin() + std::min<int64_t>(max_out, int64_t(pts.size())), out);
 }
 
 }  // namespace spimdecon
@@ -518,6 +666,12 @@ extern "C" void spim_dog_params_default(spim_dog_params* p) {
     p->max_intensity = std::nan("");
     p->ij_threads = 8;
     p->device = 0;
+}
+
+extern "C" int spim_dog_interest_points(const float* img, const int64_t* dims, const spim_dog_params* p,
+                                        float* dog_out, spim_interest_point* out, int64_t max_out,
+                                        int64_t* nout) {
+    return guarded([&] { dog_interest_points(img, dims, p, dog_out, out, max_out, nout); });
 }
 
 extern "C" int spim_dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p,

@@ -1,9 +1,9 @@
 """Host-side mirror of the DoG bead-detection pass (ProcessDOG.compute).
 
-spim/process/interestpointdetection/ProcessDOG.java:40-178 and
-Localization.noLocalization (Localization.java:19-45); the whole pass
-(min/max, normalisation, both Gaussians, subtraction, 26-neighbour peak
-test, compaction) runs on the GPU in ``spim_dog_compute``.
+spim/process/interestpointdetection/ProcessDOG.java:40-178 and Localization
+(Localization.java:19-88: none, or the quadratic sub-pixel fit); the whole
+pass (min/max, normalisation, both Gaussians, subtraction, 26-neighbour peak
+test, compaction, fit) runs on the GPU in ``spim_dog_interest_points``.
 """
 from __future__ import annotations
 
@@ -52,21 +52,44 @@ def compute(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, local
     dims = (C.c_int64 * 3)(img.shape[2], img.shape[1], img.shape[0])
     dog = np.empty_like(img) if return_dog else None
     cap = int(max_peaks) if max_peaks is not None else max(1024, img.size // 64)
-    peaks = (_lib.Peak * cap)()
+    pts = (_lib.InterestPointC * cap)()
     n = C.c_int64(0)
-    check(lib.spim_dog_compute(fptr(img), dims, C.byref(p), fptr(dog) if dog is not None else None,
-                               peaks, cap, C.byref(n)))
+    dptr = fptr(dog) if dog is not None else None
+    check(lib.spim_dog_interest_points(fptr(img), dims, C.byref(p), dptr, pts, cap, C.byref(n)))
     total = int(n.value)
     if total > cap:   # rerun with the exact capacity
-        peaks = (_lib.Peak * total)()
-        check(lib.spim_dog_compute(fptr(img), dims, C.byref(p), fptr(dog) if dog is not None else None,
-                                   peaks, total, C.byref(n)))
+        pts = (_lib.InterestPointC * total)()
+        check(lib.spim_dog_interest_points(fptr(img), dims, C.byref(p), dptr, pts, total, C.byref(n)))
     out = []
-    for i in range(min(total, len(peaks))):
-        pk = peaks[i]
-        loc = (float(pk.x), float(pk.y), float(pk.z))
-        out.append(InterestPoint(i, loc, float(pk.intensity) if keep_intensity else None))
+    for i in range(min(total, len(pts))):
+        ip = pts[i]
+        out.append(InterestPoint(i, (ip.pos[0], ip.pos[1], ip.pos[2]),
+                                 float(ip.intensity) if keep_intensity else None))
     return (out, dog) if return_dog else out
+
+
+def simple_peaks(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, localization: int = 0,
+                 image_sigma=(0.5, 0.5, 0.5), find_min: bool = False, find_max: bool = True,
+                 min_intensity: float = float("nan"), max_intensity: float = float("nan"),
+                 device: int = 0, ij_threads: int = 8):
+    """DifferenceOfGaussianNewPeakFinder.getSimplePeaks: [(x, y, z, |v|, is_min, is_max)]
+    (threshold / 10 when ``localization`` is 1)."""
+    lib = _lib.load()
+    img = np.ascontiguousarray(img, np.float32)
+    p = _lib.DogParams()
+    lib.spim_dog_params_default(C.byref(p))
+    p.sigma, p.threshold, p.localization = float(sigma), float(threshold), int(localization)
+    for d in range(3):
+        p.image_sigma[d] = float(image_sigma[d])
+    p.find_min, p.find_max = int(bool(find_min)), int(bool(find_max))
+    p.min_intensity, p.max_intensity = float(min_intensity), float(max_intensity)
+    p.ij_threads, p.device = int(ij_threads), int(device)
+    dims = (C.c_int64 * 3)(img.shape[2], img.shape[1], img.shape[0])
+    n = C.c_int64(0)
+    check(lib.spim_dog_compute(fptr(img), dims, C.byref(p), None, None, 0, C.byref(n)))
+    pk = (_lib.Peak * max(int(n.value), 1))()
+    check(lib.spim_dog_compute(fptr(img), dims, C.byref(p), None, pk, int(n.value), C.byref(n)))
+    return [(q.x, q.y, q.z, q.intensity, bool(q.is_min), bool(q.is_max)) for q in pk[:int(n.value)]]
 
 
 def peaks_array(points) -> np.ndarray:

@@ -47,3 +47,33 @@ def test_dog_flat_image_has_no_peaks_and_no_nan(gpu):
     exp, dref = dog_ref.process_dog(img)
     np.testing.assert_array_equal(d, dref)
     assert len(pts) == len(exp)
+
+
+@pytest.mark.parametrize("find_min,find_max", [(False, True), (True, True)])
+def test_dog_quadratic_localization(gpu, find_min, find_max):
+    """Localization 1 (the reference's default, DifferenceOf.java:46): candidates at
+    threshold/10, quadratic sub-pixel fit, |fitted value| > threshold."""
+    img = bead_stack(cid=13)
+    pts, d = dog.compute(img, sigma=1.8, threshold=0.008, localization=1, find_min=find_min,
+                         find_max=find_max, return_dog=True, keep_intensity=True)
+    exp, dref = dog_ref.process_dog(img, 1.8, 0.008, localization=1, find_min=find_min,
+                                    find_max=find_max)
+    np.testing.assert_array_equal(d, dref)
+    assert len(pts) == len(exp) and len(exp) > 10
+    got = np.array([p.location for p in pts])
+    want = np.array([e[:3] for e in exp])
+    # identical double arithmetic; float32-rounded positions
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-5)
+    np.testing.assert_allclose([p.intensity for p in pts], [e[3] for e in exp], rtol=1e-6, atol=1e-9)
+    assert np.any(np.abs(got - np.round(got)) > 1e-3)      # genuinely sub-pixel
+
+
+def test_dog_simple_peaks_threshold_tenth(gpu):
+    """getSimplePeaks at localization 1 uses threshold / 10 (ProcessDOG.java:63-67)."""
+    img = bead_stack(shape=(24, 26, 30), cid=14)
+    p0 = dog.simple_peaks(img, threshold=0.008, localization=0)
+    p1 = dog.simple_peaks(img, threshold=0.008, localization=1)
+    _, dref = dog_ref.process_dog(img, 1.8, 0.008)
+    e1 = dog_ref.find_peaks(dref, float(np.float32(0.008) / np.float32(10.0)))
+    assert len(p1) >= len(p0)
+    assert [q[:3] for q in p1] == [e[:3] for e in e1 if e[5]]

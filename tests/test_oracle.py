@@ -171,3 +171,18 @@ def test_find_peaks_order_and_labels():
     assert [(q[0], q[4], q[5]) for q in p] == [(2, False, True), (6, True, False)]
     p2 = dog_ref.find_peaks(d, 0.5, ij_threads=3)   # x%3: 6->0 first, 2->2
     assert [q[0] for q in p2] == [6, 2]
+
+
+def test_quadratic_localization_recovers_paraboloid_vertex():
+    """A sampled paraboloid has its exact vertex as the quadratic fit; starting one
+    voxel off, the fit moves (LaPlaceFunctions.java:94-119) and converges."""
+    z, y, x = np.mgrid[0:12, 0:13, 0:14].astype(np.float64)
+    x0, y0, z0 = 6.3, 5.8, 7.4
+    f = (-(1 - ((x - x0) ** 2 + 2 * (y - y0) ** 2 + 3 * (z - z0) ** 2) / 50)).astype(np.float32)
+    for start in [(6, 6, 7, 0.9), (8, 5, 7, 0.5), (5, 7, 8, 0.5)]:
+        (px, py, pz, v), = dog_ref.quadratic_localization(f, [start])
+        assert abs(px - x0) < 1e-4 and abs(py - y0) < 1e-4 and abs(pz - z0) < 1e-4
+        assert abs(v + 1.0) < 1e-5
+    # flat neighbourhood: singular Hessian -> the peak stays as detected
+    flat = np.zeros((5, 5, 5), np.float32)
+    assert dog_ref.quadratic_localization(flat, [(2, 2, 2, 0.25)]) == [(2.0, 2.0, 2.0, np.float32(0.25))]
