@@ -17,12 +17,26 @@ namespace {
 
 // ------------------------------------------------------------------ small helpers
 
+// The FFT arithmetic below may contract into FMAs (the build is -ffp-contract=off
+// so that the RL pointwise steps keep the reference's float op order; those use
+// explicit __f*_rn intrinsics).  The spectra are not bit-matched to any
+// reference anyway, and FMA is the more accurate of the two.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+#pragma clang fp contract(fast)
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+#pragma clang fp contract(fast)
+    return make_float2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+#pragma clang fp contract(fast)
+    return make_float2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) {
+#pragma clang fp contract(fast)
+    return make_float2(a.x * s, a.y * s);
+}
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
@@ -52,6 +66,22 @@ __device__ __forceinline__ float next_value(float last, float integral, float we
             adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
         else
             adjusted = value;
+    } else {
+        adjusted = kMinValue;
+    }
+    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
+    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
+}
+
+// Same with lambda's sign known at compile time: the Tikhonov branch (double
+// sqrt / divide) is not even if-converted into the lambda = 0 kernels.
+template <bool TIK>
+__device__ __forceinline__ float next_value_t(float last, float integral, float weight, double lambda) {
+    const float value = __fmul_rn(last, integral);
+    float adjusted;
+    if (value > 0.0f) {
+        if constexpr (TIK) adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
+        else adjusted = value;
     } else {
         adjusted = kMinValue;
     }
@@ -510,14 +540,16 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const unsigned grid = unsigned(std::min<int64_t>({ntiles, 256 * per_cu, 4096}));
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
-#define SD_XT(SV, A, B)                                                                               \
-    if (!done && sv == SV && L == (A) * (B)) {                                                       \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B>),         \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));           \
-        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B>), dim3(grid), dim3(kXtThreads), lds, s, b);     \
-        done = true;                                                                                 \
+    const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
+#define SD_XT(SV, A, B, TK)                                                                             \
+    if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                            \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK>),       \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
+        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK>), dim3(grid), dim3(kXtThreads), lds, s, b);   \
+        done = true;                                                                                   \
     }
-#define SD_XT_S(A, B) SD_XT(0, A, B) SD_XT(1, A, B)
+#define SD_XT_S(A, B) \
+    SD_XT(0, A, B, false) SD_XT(1, A, B, false) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true) SD_XT(1, A, B, true) }
     SD_X2F_SIZES(SD_XT_S)
 #undef SD_XT_S
 #undef SD_XT
@@ -591,27 +623,26 @@ int col_tx(int L) {
 // two-factor column pass; false when the buffer-offset path does not apply
 template <int AXIS, int MODE>
 bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+    const int TX = k2fTX;  // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
     const int L = f.L;
-    const size_t lds = size_t(L * k2fTX + L) * sizeof(float2);
+    const size_t lds = size_t(L * TX + L) * sizeof(float2);
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
     if (lds > 80 * 1024 || bytes >= (uint64_t(1) << 31)) return false;
-    const int64_t ntiles = (p.Hp / k2fTX) * (AXIS == 1 ? p.g.Mz : p.g.My);
-    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * 2 * 4));
-    // the fused z pass keeps the larger factor in phases A/C and multiplies by K
-    // on the smaller one (phase B), which bounds its registers
-    const int n1 = MODE == 2 ? std::min(f.n1, f.n2) : f.n1;
-    const int n2 = MODE == 2 ? std::max(f.n1, f.n2) : f.n2;
+    const int64_t ntiles = (p.Hp / TX) * (AXIS == 1 ? p.g.Mz : p.g.My);
+    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * 4));
+    const int n1 = f.n1, n2 = f.n2;
     bool done = false;
-#define SD_2F_C1(A, B)                                                                                   \
-    if (!done && n1 == (A) && n2 == (B)) {                                                               \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE>),           \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));               \
-        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE>), dim3(grid), dim3(k2fColThreads), lds, s, p.g,   \
-                           p.Hp, f.tw, C, K, uint32_t(bytes));                                           \
-        done = true;                                                                                     \
+#define SD_2F_C1(A, B, T)                                                                                  \
+    if (!done && n1 == (A) && n2 == (B) && TX == (T)) {                                                    \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T>),         \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
+        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T>), dim3(grid), dim3(T * 32), lds, s, p.g, p.Hp,   \
+                           f.tw, C, K, uint32_t(bytes));                                                   \
+        done = true;                                                                                       \
     }
 #define SD_2F_C(A, B) \
-    if constexpr (MODE == 2) { SD_2F_C1((A < B ? A : B), (A < B ? B : A)) } else { SD_2F_C1(A, B) }
+    SD_2F_C1(A, B, 16)
     SD_2F_SIZES(SD_2F_C)
 #undef SD_2F_C
 #undef SD_2F_C1
