@@ -620,6 +620,17 @@ int col_tx(int L) {
     fail(SPIMDECON_ERR_ARG, "column FFT length " + std::to_string(L) + " exceeds the LDS tile");
 }
 
+// blocks per resident slot of the column passes (grid-stride tiles); env
+// SPIMDECON_COLGRID overrides for A/B runs
+static int col_grid_rounds() {
+    static const int r = [] {
+        const char* e = std::getenv("SPIMDECON_COLGRID");
+        return e ? std::max(1, std::atoi(e)) : 4;
+    }();
+    return r;
+}
+#define kColGridRounds col_grid_rounds()
+
 // two-factor column pass; false when the buffer-offset path does not apply
 template <int AXIS, int MODE>
 bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
@@ -630,7 +641,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     if (lds > 80 * 1024 || bytes >= (uint64_t(1) << 31)) return false;
     const int64_t ntiles = (p.Hp / TX) * (AXIS == 1 ? p.g.Mz : p.g.My);
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * 4));
+    const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
     const int n1 = f.n1, n2 = f.n2;
     bool done = false;
 #define SD_2F_C1(A, B, T)                                                                                  \
@@ -780,6 +791,8 @@ void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
 }
 
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s) {
+    // fused forward * K * inverse (0.57 ms at 540^3) beat forward z + (C*K) inverse z
+    // as two launches (0.61 ms)
     if (K) launch_col<2, false, 1>(p, p.fz, C, K, s);
     else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
 }
