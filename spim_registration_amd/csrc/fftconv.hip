@@ -240,7 +240,14 @@ struct XArgs {
     float kscale;
     uint32_t spec_bytes;  // k_xrows buffer ranges (< 2 GiB each)
     uint32_t nvox;
+    // packed row pairs processed by this launch: [pb0, pb0 + pn0) then [pb1, pb1 + pn1)
+    int pb0, pn0, pb1, pn1;
 };
+
+// linear index of a launch -> packed row pair (-1 past the ranges)
+__device__ __forceinline__ int x_pair(const XArgs& a, int i) {
+    return i < a.pn0 ? a.pb0 + i : (i - a.pn0 < a.pn1 ? a.pb1 + (i - a.pn0) : -1);
+}
 
 constexpr int kXThreads = 256;             // four waves; one packed row pair per wave
 constexpr int kXPairs = kXThreads / 64;
@@ -264,13 +271,13 @@ __global__ __launch_bounds__(kXThreads) void k_xpass(XArgs a) {
     float2* B = A + Mx + 2;
     for (int i = threadIdx.x; i < Mx; i += kXThreads) tw[i] = a.fx.tw[i];
     const int nrows = int(g.My * g.Mz);
-    const int npairs = (nrows + 1) / 2;
+    const int nlin = a.pn0 + a.pn1;
     double ssum = 0.0;
     float smax = -1.0f;
     __syncthreads();
-    for (int pg = blockIdx.x; pg * kXPairs < npairs; pg += gridDim.x) {
-        const int pair = pg * kXPairs + wv;
-        const bool active = pair < npairs;
+    for (int pg = blockIdx.x; pg * kXPairs < nlin; pg += gridDim.x) {
+        const int pair = x_pair(a, pg * kXPairs + wv);
+        const bool active = pair >= 0;
         const int r0 = 2 * pair, r1 = 2 * pair + 1;
         const bool valid0 = active && r0 < nrows, valid1 = active && r1 < nrows;
         const int sm0 = valid0 ? a.row_mirror[r0] : -1, sm1 = valid1 ? a.row_mirror[r1] : -1;
@@ -485,15 +492,18 @@ size_t x_lds(const SpectralPlan& p) {
 
 // x-pass grid, shared by k_xpass and k_xrows (also the number of stats
 // partials an update pass writes)
-unsigned x_grid(const SpectralPlan& p) {
-    const int64_t nrows = p.g.My * p.g.Mz;
-    const int64_t npairs = (nrows + 1) / 2;
-    int64_t b = ceil_div(npairs, kXPairs);
-    return unsigned(std::min<int64_t>(b, 256 * 8));
+unsigned x_grid(const XArgs& a) {
+    const int64_t b = ceil_div(int64_t(a.pn0) + a.pn1, kXPairs);
+    return unsigned(std::max<int64_t>(1, std::min<int64_t>(b, 256 * 8)));
 }
 
 XArgs base_args(const SpectralPlan& p) {
     XArgs a{};
+    SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
+    a.pb0 = 0;
+    a.pn0 = int((p.g.My * p.g.Mz + 1) / 2);
+    a.pb1 = 0;
+    a.pn1 = 0;
     a.g = p.g;
     a.Hx = p.Hx;
     a.Hp = p.Hp;
@@ -534,8 +544,7 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const int L = int(p.g.Mx);
     const size_t lds = size_t(L + 1 + kXtPairs * (L + 1)) * sizeof(float2);
     if (lds > 160 * 1024) return 0;
-    const int64_t npairs = (p.g.My * p.g.Mz + 1) / 2;
-    const int64_t ntiles = ceil_div(npairs, kXtPairs);
+    const int64_t ntiles = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, kXtPairs));
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
     const unsigned grid = unsigned(std::min<int64_t>({ntiles, 256 * per_cu, 4096}));
     const int sv = st == Store::F32 ? 0 : 1;
@@ -570,7 +579,7 @@ unsigned launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const size_t lds = size_t(Mx + kXPairs * xrows_wave_elems(Mx, false)) * sizeof(float2);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
     SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
-    const unsigned grid = x_grid(p);
+    const unsigned grid = x_grid(a);
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
 #define SD_XR(SV, UU, VV)                                                                               \
@@ -600,7 +609,7 @@ unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s
     const size_t lds = x_lds(p);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
     SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
-    const unsigned grid = x_grid(p);
+    const unsigned grid = x_grid(a);
     if (st == Store::F32) {
         SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xpass<MODE, 0>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
@@ -797,9 +806,19 @@ void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t
     else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
 }
 
+PairRanges all_pairs(const SpectralPlan& p) {
+    PairRanges r;
+    r.n0 = int((p.g.My * p.g.Mz + 1) / 2);
+    return r;
+}
+
 void engine_quotient(const SpectralPlan& p, Store st, const float2* Cin, const void* img,
-                     float2* Cout, hipStream_t s) {
+                     float2* Cout, const PairRanges& pr, hipStream_t s) {
     XArgs a = base_args(p);
+    a.pb0 = pr.b0;
+    a.pn0 = pr.n0;
+    a.pb1 = pr.b1;
+    a.pn1 = pr.n1;
     a.Cin = Cin;
     a.Cout = Cout;
     a.img = img;
@@ -808,8 +827,12 @@ void engine_quotient(const SpectralPlan& p, Store st, const float2* Cin, const v
 
 int64_t engine_update(const SpectralPlan& p, Store st, const float2* Cin, const float* psi_in,
                       const void* w, double lambda, float* psi_out, float2* Cout, double* partials,
-                      hipStream_t s) {
+                      const PairRanges& pr, hipStream_t s) {
     XArgs a = base_args(p);
+    a.pb0 = pr.b0;
+    a.pn0 = pr.n0;
+    a.pb1 = pr.b1;
+    a.pn1 = pr.n1;
     a.Cin = Cin;
     a.Cout = Cout;
     a.psi_in = psi_in;

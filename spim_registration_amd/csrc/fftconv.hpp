@@ -68,14 +68,22 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 // Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
+// packed row pairs (rows 2i, 2i+1 of the My*Mz padded rows) an x pass covers:
+// [b0, b0 + n0) then [b1, b1 + n1)
+struct PairRanges {
+    int b0 = 0, n0 = 0, b1 = 0, n1 = 0;
+};
+// all packed row pairs of a slab
+PairRanges all_pairs(const SpectralPlan& p);
+
 // X pass A: conv1 result (Cin) -> quotient with img -> forward spectrum into Cout
 void engine_quotient(const SpectralPlan& p, Store st, const float2* Cin, const void* img,
-                     float2* Cout, hipStream_t s);
+                     float2* Cout, const PairRanges& pr, hipStream_t s);
 // X pass B: conv2 result (Cin) -> update psi_in -> psi_out, forward spectrum of the
 // mirror-extended psi_out into Cout (when Cout != nullptr); stats partials (2 doubles / block).
 // returns the number of partials written
 int64_t engine_update(const SpectralPlan& p, Store st, const float2* Cin, const float* psi_in,
                       const void* w, double lambda, float* psi_out, float2* Cout, double* partials,
-                      hipStream_t s);
+                      const PairRanges& pr, hipStream_t s);
 
 }  // namespace spimdecon

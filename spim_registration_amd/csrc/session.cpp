@@ -38,6 +38,9 @@ Session::Session(const mvd_params& p) : p_(p) {
     SD_CHECK(backend_ == 0 || backend_ == 1, SPIMDECON_ERR_ARG, "unknown fft_backend");
     DeviceGuard guard(p.device);
     SD_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    SD_HIP(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking));
+    SD_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
+    SD_HIP(hipEventCreateWithFlags(&ev_x_, hipEventDisableTiming));
     if (p_.nranks > 1) {
         ncclUniqueId id;
         std::memcpy(&id, p_.comm_id, sizeof(id));
@@ -69,7 +72,11 @@ Session::~Session() {
     for (auto e : event_pool_) (void)hipEventDestroy(e);
     slabs_.clear();
     stats_dev_.release();
+    if (xstream_) (void)hipStreamSynchronize(xstream_);
     if (comm_) ncclCommDestroy(comm_);
+    if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
+    if (ev_x_) (void)hipEventDestroy(ev_x_);
+    if (xstream_) (void)hipStreamDestroy(xstream_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -281,18 +288,18 @@ hipEvent_t Session::get_event() {
     return e;
 }
 
-void Session::tstart(int cls) {
+void Session::tstart(int cls, hipStream_t st) {
     if (!timing_on_) return;
     TimingRec r{cls, get_event(), nullptr};
-    SD_HIP(hipEventRecord(r.a, stream_));
+    SD_HIP(hipEventRecord(r.a, st ? st : stream_));
     trecs_.push_back(r);
     tcur_ = int(trecs_.size()) - 1;
 }
 
-void Session::tstop() {
+void Session::tstop(hipStream_t st) {
     if (!timing_on_ || tcur_ < 0) return;
     trecs_[tcur_].b = get_event();
-    SD_HIP(hipEventRecord(trecs_[tcur_].b, stream_));
+    SD_HIP(hipEventRecord(trecs_[tcur_].b, st ? st : stream_));
     tcur_ = -1;
 }
 
@@ -300,55 +307,73 @@ void Session::timing(double* out16) {
     for (int i = 0; i < 16; ++i) out16[i] = tacc_[i];
 }
 
-void Session::exchange(bool buffer_a) {
+void Session::exchange(bool buffer_a, hipStream_t st) {
     if (backend_ == 1) {
         exchange_planes([](SlabState& sl, bool a) { return a ? sl.Ra.p : sl.Rb.p; }, buffer_a,
-                        size_t(slabs_[0].g.Sx * slabs_[0].g.My));
+                        size_t(slabs_[0].g.Sx * slabs_[0].g.My), st);
     } else {
         exchange_planes(
             [](SlabState& sl, bool a) { return reinterpret_cast<float*>(a ? sl.C1.p : sl.C2.p); },
-            buffer_a, size_t(2 * slabs_[0].sp.Hp * slabs_[0].g.My));
+            buffer_a, size_t(2 * slabs_[0].sp.Hp * slabs_[0].g.My), st);
     }
 }
 
+bool Session::split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest) const {
+    const int64_t My = sl.g.My, nz = sl.g.nz, cz = halo_[2];
+    const int64_t npairs = (My * sl.g.Mz + 1) / 2;
+    const int64_t e1 = ceil_div(cz * My, int64_t(2));   // pairs holding planes [0, cz)
+    const int64_t s2 = ((nz - cz) * My) / 2;            // ... planes [nz - cz, nz)
+    const int64_t e2 = ceil_div(nz * My, int64_t(2));
+    if (cz <= 0 || s2 < e1) return false;
+    bnd.b0 = 0;
+    bnd.n0 = int(e1);
+    bnd.b1 = int(s2);
+    bnd.n1 = int(e2 - s2);
+    rest.b0 = int(e1);
+    rest.n0 = int(s2 - e1);
+    rest.b1 = int(e2);
+    rest.n1 = int(npairs - e2);
+    return true;
+}
+
 // halo exchange of cz padded z-planes between neighbouring slabs (local copies and RCCL)
-void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane) {
+void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane, hipStream_t st) {
     const int S = int(slabs_.size());
     if (S == 1 && p_.nranks == 1) return;
     const int cz = halo_[2];
     if (cz <= 0) return;
-    tstart(5);
+    tstart(5, st);
     const size_t bytes = size_t(cz) * plane * sizeof(float);
     for (int s = 1; s < S; ++s) {
         SlabState& lo = slabs_[s - 1];
         SlabState& hi = slabs_[s];
         // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
         SD_HIP(hipMemcpyAsync(get(lo, which) + size_t(lo.g.nz) * plane, get(hi, which), bytes,
-                              hipMemcpyDeviceToDevice, stream_));
+                              hipMemcpyDeviceToDevice, st));
         // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
         SD_HIP(hipMemcpyAsync(get(hi, which) + size_t(hi.g.Mz - cz) * plane,
                               get(lo, which) + size_t(lo.g.nz - cz) * plane, bytes,
-                              hipMemcpyDeviceToDevice, stream_));
+                              hipMemcpyDeviceToDevice, st));
     }
     if (p_.nranks > 1) {
         const size_t count = size_t(cz) * plane;
         SD_NCCL(ncclGroupStart());
         if (p_.rank > 0) {
             SlabState& s0 = slabs_[0];
-            SD_NCCL(ncclSend(get(s0, which), count, ncclFloat, p_.rank - 1, comm_, stream_));
+            SD_NCCL(ncclSend(get(s0, which), count, ncclFloat, p_.rank - 1, comm_, st));
             SD_NCCL(ncclRecv(get(s0, which) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
-                             p_.rank - 1, comm_, stream_));
+                             p_.rank - 1, comm_, st));
         }
         if (p_.rank < p_.nranks - 1) {
             SlabState& sl = slabs_[S - 1];
             SD_NCCL(ncclSend(get(sl, which) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
-                             p_.rank + 1, comm_, stream_));
+                             p_.rank + 1, comm_, st));
             SD_NCCL(ncclRecv(get(sl, which) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
-                             comm_, stream_));
+                             comm_, st));
         }
         SD_NCCL(ncclGroupEnd());
     }
-    tstop();
+    tstop(st);
 }
 
 void Session::allreduce_sum(double* host, int n) {
@@ -416,7 +441,7 @@ void Session::run_rocfft(int iters, double lambda) {
         launch_pad_mirror(sl.g, sl.psi, sl.Ra.p, stream_);
         tstop();
     }
-    exchange(true);
+    exchange(true, stream_);
     for (int it = 0; it < iters; ++it) {
         for (int v = 0; v < V; ++v) {
             const bool last = (it == iters - 1) && (v == V - 1);
@@ -426,7 +451,7 @@ void Session::run_rocfft(int iters, double lambda) {
                 tstart(4); sl.fft->inverse(sl.Ra.p); tstop();
                 tstart(1); launch_quotient_pad(sl.g, store_, sl.img[v].p, sl.Ra.p, sl.Rb.p, stream_); tstop();
             }
-            exchange(false);
+            exchange(false, stream_);
             for (size_t s = 0; s < slabs_.size(); ++s) {  // convolve2 + update
                 SlabState& sl = slabs_[s];
                 tstart(2); sl.fft->forward(sl.Rb.p); tstop();
@@ -442,7 +467,7 @@ void Session::run_rocfft(int iters, double lambda) {
                 tstop();
                 std::swap(sl.psi, sl.psi_next);
             }
-            if (!last) exchange(true);
+            if (!last) exchange(true, stream_);
         }
     }
 }
@@ -451,39 +476,91 @@ void Session::run_rocfft(int iters, double lambda) {
 // 4 initial psi x-pass, 5 halo exchange, 6 stats reduce
 void Session::run_engine(int iters, double lambda) {
     const int V = nviews_;
+    const bool halo = slabs_.size() > 1 || p_.nranks > 1;
+    // overlap: the x pass writes the planes the neighbours need first; their exchange
+    // (xstream_) runs while the x pass covers the rest of the slab
+    std::vector<PairRanges> bnd(slabs_.size()), rest(slabs_.size());
+    bool overlap = halo;
+    for (size_t s = 0; s < slabs_.size(); ++s)
+        overlap = overlap && split_pairs(slabs_[s], bnd[s], rest[s]);
+    auto start_exchange = [&](bool buffer_a) {  // after the boundary launches on stream_
+        SD_HIP(hipEventRecord(ev_bnd_, stream_));
+        SD_HIP(hipStreamWaitEvent(xstream_, ev_bnd_, 0));
+        exchange(buffer_a, xstream_);
+        SD_HIP(hipEventRecord(ev_x_, xstream_));
+    };
+    auto finish_exchange = [&]() { SD_HIP(hipStreamWaitEvent(stream_, ev_x_, 0)); };
+
     for (auto& sl : slabs_) {
         tstart(4);
         engine_forward_psi(sl.sp, sl.psi, sl.C1.p, stream_);
         tstop();
     }
-    exchange(true);
+    exchange(true, stream_);
     for (int it = 0; it < iters; ++it) {
         for (int v = 0; v < V; ++v) {
             const bool last = (it == iters - 1) && (v == V - 1);
-            for (auto& sl : slabs_) {                    // convolve1 + quotient
+            for (auto& sl : slabs_) {  // convolve1
                 tstart(2); engine_ypass(sl.sp, sl.C1.p, false, stream_); tstop();
                 tstart(3); engine_zpass(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_); tstop();
                 tstart(2); engine_ypass(sl.sp, sl.C1.p, true, stream_); tstop();
-                tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, stream_); tstop();
             }
-            exchange(false);
-            for (size_t s = 0; s < slabs_.size(); ++s) {  // convolve2 + update (+ next forward x)
-                SlabState& sl = slabs_[s];
+            // quotient (+ forward x of the quotient) and its halo exchange
+            if (overlap) {
+                for (size_t s = 0; s < slabs_.size(); ++s) {
+                    SlabState& sl = slabs_[s];
+                    tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, bnd[s], stream_); tstop();
+                }
+                start_exchange(false);
+                for (size_t s = 0; s < slabs_.size(); ++s) {
+                    SlabState& sl = slabs_[s];
+                    tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, rest[s], stream_); tstop();
+                }
+                finish_exchange();
+            } else {
+                for (auto& sl : slabs_) {
+                    tstart(1);
+                    engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, all_pairs(sl.sp), stream_);
+                    tstop();
+                }
+                exchange(false, stream_);
+            }
+            for (auto& sl : slabs_) {  // convolve2
                 tstart(2); engine_ypass(sl.sp, sl.C2.p, false, stream_); tstop();
                 tstart(3); engine_zpass(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_); tstop();
                 tstart(2); engine_ypass(sl.sp, sl.C2.p, true, stream_); tstop();
+            }
+            // update (+ forward x of the next psi) and its halo exchange
+            const bool ov = overlap && !last;
+            std::vector<int64_t> nb(slabs_.size(), 0);
+            for (size_t s = 0; s < slabs_.size(); ++s) {
+                SlabState& sl = slabs_[s];
                 tstart(0);
-                const int64_t nb = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda,
-                                                 sl.psi_next, last ? nullptr : sl.C1.p, sl.partials.p,
-                                                 stream_);
+                nb[s] = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
+                                      last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp),
+                                      stream_);
                 tstop();
+            }
+            if (ov) {
+                start_exchange(true);
+                for (size_t s = 0; s < slabs_.size(); ++s) {
+                    SlabState& sl = slabs_[s];
+                    tstart(0);
+                    nb[s] += engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
+                                           sl.C1.p, sl.partials.p + 2 * nb[s], rest[s], stream_);
+                    tstop();
+                }
+            }
+            for (size_t s = 0; s < slabs_.size(); ++s) {
+                SlabState& sl = slabs_[s];
                 tstart(6);
-                launch_reduce_partials(sl.partials.p, nb, stats_dev_.p + (size_t(it) * V + v) * 2,
+                launch_reduce_partials(sl.partials.p, nb[s], stats_dev_.p + (size_t(it) * V + v) * 2,
                                        s > 0 ? 1 : 0, stream_);
                 tstop();
                 std::swap(sl.psi, sl.psi_next);
             }
-            if (!last) exchange(true);
+            if (ov) finish_exchange();
+            else if (!last) exchange(true, stream_);
         }
     }
 }

@@ -72,19 +72,23 @@ public:
 
 private:
     void build_spectra();
-    void exchange(bool buffer_a);
-    void exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane_floats);
+    void exchange(bool buffer_a, hipStream_t st);
+    void exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane_floats, hipStream_t st);
+    // x-pass pair ranges of a slab: the planes its neighbours need (bnd) and the rest
+    bool split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest) const;
     void run_rocfft(int iters, double lambda);
     void run_engine(int iters, double lambda);
     void allreduce_sum(double* host, int n);
     void allreduce_max(double* host, int n);
-    void tstart(int cls);
-    void tstop();
+    void tstart(int cls, hipStream_t st = nullptr);
+    void tstop(hipStream_t st = nullptr);
 
     mvd_params p_{};
     int backend_ = 0;  // 0 = fused spectral engine, 1 = rocFFT (mvd_params.fft_backend)
     Store store_ = Store::F32;
     hipStream_t stream_ = nullptr;
+    hipStream_t xstream_ = nullptr;  // halo exchanges overlapped with the interior x pass
+    hipEvent_t ev_bnd_ = nullptr, ev_x_ = nullptr;
     ncclComm_t comm_ = nullptr;
     std::vector<SlabState> slabs_;
     std::vector<HostKernel> k1_, k2_;
