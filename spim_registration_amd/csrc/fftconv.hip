@@ -673,6 +673,13 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
 
 template <int AXIS, bool INV, int ZMODE>
 void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+    static const bool zk_lds = [] {  // SPIMDECON_ZK=reg: kernel spectrum in phase-B registers (A/B)
+        const char* e = std::getenv("SPIMDECON_ZK");
+        return !(e && e[0] == 'r');
+    }();
+    if constexpr (ZMODE == 1) {
+        if (f.n1 && zk_lds && launch_col2f<AXIS, 4>(p, f, C, K, s)) return;
+    }
     if (f.n1 && launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s)) return;
     const int tx = col_tx(f.L);
     SD_CHECK(f.L * tx / 2 <= kColMaxU * kCThreads, SPIMDECON_ERR_ARG, "column tile exceeds prefetch registers");
