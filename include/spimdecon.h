@@ -260,6 +260,47 @@ int spim_dog_interest_points(const float* img, const int64_t* dims, const spim_d
                              float* dog_out, spim_interest_point* out, int64_t max_out,
                              int64_t* nout);
 
+/* ======================================================================
+ * 7. Deconvolution input preparation --
+ *    spim/process/fusion/deconvolution/ProcessForDeconvolution.java:159-384:
+ *    each view resampled into the fused bounding box through the inverse of
+ *    its affine model (TransformInput(AndWeights)), cosine blending weights,
+ *    WeightNormalizer, OSEM adjustment.
+ * ====================================================================== */
+#define SPIM_WEIGHTS_NONE         0   /* WeightType.NO_WEIGHTS                          */
+#define SPIM_WEIGHTS_PRECOMPUTED  1   /* WeightType.PRECOMPUTED_WEIGHTS                 */
+#define SPIM_WEIGHTS_VIRTUAL      2   /* WeightType.VIRTUAL_WEIGHTS (the default)       */
+
+typedef struct spim_view_source {
+    const float* img;        /* source stack, x-fastest {nx, ny, nz}                     */
+    int64_t      dims[3];
+    double       model[12];  /* row-major 3x4 affine, source -> world (ViewRegistration)  */
+} spim_view_source;
+
+typedef struct spim_input_params {
+    int64_t bb_min[3];           /* bounding box of the fused volume (world voxels)       */
+    int64_t bb_dims[3];
+    float   blending_border[3];  /* default -8 (EfficientBayesianBased.java:76)          */
+    float   blending_range[3];   /* default 12 (EfficientBayesianBased.java:75)           */
+    int     weight_type;         /* SPIM_WEIGHTS_*                                         */
+    int     osem_index;          /* 0: osem_speedup, 1: min, 2: average overlapping views  */
+    double  osem_speedup;
+    int     ij_threads;          /* portions of the overlap statistics (2T)               */
+    int     device;
+    int     src_on_device;       /* 1: views[].img are device pointers                    */
+    int     out_on_device;       /* 1: img_out / weight_out are device pointers           */
+    int     reserved[8];
+} spim_input_params;
+
+void spim_input_params_default(spim_input_params* p);
+
+/* img_out[v], weight_out[v]: bb_dims voxels each (x-fastest).  osem_used,
+ * min_overlap, avg_overlap (may be NULL) report the OSEM factor applied and
+ * WeightNormalizer's overlap statistics (-1 / NaN for SPIM_WEIGHTS_NONE). */
+int spim_prepare_inputs(int nviews, const spim_view_source* views, const spim_input_params* p,
+                        float* const* img_out, float* const* weight_out, double* osem_used,
+                        int* min_overlap, double* avg_overlap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,18 @@ class Peak(C.Structure):
                 ("intensity", C.c_float), ("is_min", C.c_int32), ("is_max", C.c_int32)]
 
 
+class ViewSource(C.Structure):
+    _fields_ = [("img", C.POINTER(C.c_float)), ("dims", C.c_int64 * 3), ("model", C.c_double * 12)]
+
+
+class InputParams(C.Structure):
+    _fields_ = [("bb_min", C.c_int64 * 3), ("bb_dims", C.c_int64 * 3),
+                ("blending_border", C.c_float * 3), ("blending_range", C.c_float * 3),
+                ("weight_type", C.c_int), ("osem_index", C.c_int), ("osem_speedup", C.c_double),
+                ("ij_threads", C.c_int), ("device", C.c_int), ("src_on_device", C.c_int),
+                ("out_on_device", C.c_int), ("reserved", C.c_int * 8)]
+
+
 class InterestPointC(C.Structure):
     _fields_ = [("pos", C.c_double * 3), ("intensity", C.c_float), ("is_max", C.c_int32)]
 
@@ -107,6 +119,10 @@ SIGNATURES = {
                                    _i64, _pi64]),
     "spim_dog_interest_points": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf,
                                            C.POINTER(InterestPointC), _i64, _pi64]),
+    "spim_input_params_default": (None, [C.POINTER(InputParams)]),
+    "spim_prepare_inputs": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(InputParams),
+                                      C.POINTER(_pf), C.POINTER(_pf), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_int), C.POINTER(C.c_double)]),
 }
 for _n in (15, 31, 63, 127):
     SIGNATURES[f"convolve_{_n}"] = SIGNATURES["convolve_7"]

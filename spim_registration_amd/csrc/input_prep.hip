@@ -1,0 +1,367 @@
+// input_prep.hip -- deconvolution input preparation on the GPU.
+//
+// Restates (paths under /root/reference/src/main/java/, DECON =
+// spim/process/fusion/deconvolution/):
+//   resampling       DECON/TransformInput.java:74-95, TransformInputAndWeights.java:86-121
+//   virtual weights  spim/process/fusion/weights/TransformedInterpolatedRealRandomAccess.java:96-118
+//   blending         spim/process/fusion/weights/BlendingRealRandomAccess.java:25-104
+//   normalisation    DECON/WeightNormalizer.java:52-205, weights/NormalizingRandomAccess.java:36-45
+//   OSEM             DECON/ProcessForDeconvolution.java:318-384
+// The imglib2 pieces absent from the container (affine inverse, applyInverse,
+// NLinearInterpolator3D) follow the restatement in oracle/input_ref.py.
+// One thread per output voxel; HBM-bound gathers (the source stack is read
+// through L2 with trilinear locality).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+#include "spimdecon.h"
+
+namespace spimdecon {
+void check_device(int dev);
+
+namespace {
+
+constexpr int kIpBlock = 256;
+
+struct AffineInv {
+    double inv[9];   // inverse of the 3x3 part, row-major
+    double tr[3];    // translation of the model
+    double full[12]; // full inverse, row-major 3x4
+};
+
+struct ViewArgs {
+    const float* src;
+    int sx, sy, sz;
+    AffineInv a;
+    float border[3], range[3];
+};
+
+__device__ __forceinline__ int mirror1(int i, int n) {
+    if (n == 1) return 0;
+    const int p = 2 * (n - 1);
+    int j = i % p;
+    if (j < 0) j += p;
+    return j >= n ? p - j : j;
+}
+
+// BlendingRealRandomAccess.computeWeight (:78-104), float arithmetic
+__device__ float blend_weight(const float t[3], const int dims[3], const float* border, const float* range,
+                              const double* lut) {
+    float w = 1.0f;
+    for (int d = 0; d < 3; ++d) {
+        const float l = t[d];
+        const float a = l - border[d];
+        const float b = (float(dims[d] - 1) - l) - border[d];
+        const float dist = fmaxf(0.0f, fminf(a, b));
+        if (dist == 0.0f) return 0.0f;
+        const float rel = dist / range[d];
+        if (rel < 1.0f) {
+            int idx = int(floor(double(rel) * 1000.0 + 0.5));
+            idx = idx < 0 ? 0 : (idx > 1000 ? 1000 : idx);
+            w = float(double(w) * lut[idx]);
+        }
+    }
+    return w;
+}
+
+// NLinearInterpolator3D on FloatType over extendMirrorSingle (restated, unpinned)
+__device__ float nlinear(const float* src, int sx, int sy, int sz, const float t[3]) {
+    const double p0 = t[0], p1 = t[1], p2 = t[2];
+    const double f0 = floor(p0), f1 = floor(p1), f2 = floor(p2);
+    const int x0 = int(f0), y0 = int(f1), z0 = int(f2);
+    const double w0 = p0 - f0, w1 = p1 - f1, w2 = p2 - f2;
+    const double i0 = 1.0 - w0, i1 = 1.0 - w1, i2 = 1.0 - w2;
+    const int xa = mirror1(x0, sx), xb = mirror1(x0 + 1, sx);
+    const int ya = mirror1(y0, sy), yb = mirror1(y0 + 1, sy);
+    const int za = mirror1(z0, sz), zb = mirror1(z0 + 1, sz);
+    auto at = [&](int x, int y, int z) { return src[(int64_t(z) * sy + y) * sx + x]; };
+    // corner order 000, 100, 110, 010, 011, 111, 101, 001
+    float acc = float(double(at(xa, ya, za)) * (i0 * i1 * i2));
+    acc = acc + float(double(at(xb, ya, za)) * (w0 * i1 * i2));
+    acc = acc + float(double(at(xb, yb, za)) * (w0 * w1 * i2));
+    acc = acc + float(double(at(xa, yb, za)) * (i0 * w1 * i2));
+    acc = acc + float(double(at(xa, yb, zb)) * (i0 * w1 * w2));
+    acc = acc + float(double(at(xb, yb, zb)) * (w0 * w1 * w2));
+    acc = acc + float(double(at(xb, ya, zb)) * (w0 * i1 * w2));
+    acc = acc + float(double(at(xa, ya, zb)) * (i0 * i1 * w2));
+    return acc;
+}
+
+__global__ __launch_bounds__(kIpBlock) void k_transform_view(ViewArgs v, int64_t bx, int64_t by, int64_t bz,
+                                                             int64_t nx, int64_t ny, int64_t n, int weight_type,
+                                                             const double* __restrict__ lut,
+                                                             float* __restrict__ img_out,
+                                                             float* __restrict__ w_out) {
+    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    // TransformInput: s = (float) position + offset; t = inv3 (s - translation)
+    const float s0 = float(x) + float(bx), s1 = float(y) + float(by), s2 = float(z) + float(bz);
+    const double d0 = double(s0) - v.a.tr[0], d1 = double(s1) - v.a.tr[1], d2 = double(s2) - v.a.tr[2];
+    float t[3];
+    for (int r = 0; r < 3; ++r)
+        t[r] = float(v.a.inv[3 * r] * d0 + v.a.inv[3 * r + 1] * d1 + v.a.inv[3 * r + 2] * d2);
+    float val = 0.0f;
+    if (t[0] >= 0.0f && t[1] >= 0.0f && t[2] >= 0.0f && t[0] < float(v.sx) && t[1] < float(v.sy) &&
+        t[2] < float(v.sz))  // FusionHelper.intersects (double compares of float values)
+        val = fmaxf(1e-4f, nlinear(v.src, v.sx, v.sy, v.sz, t));
+    img_out[i] = val;
+    const int dims[3] = {v.sx, v.sy, v.sz};
+    float w = 1.0f;
+    if (weight_type == SPIM_WEIGHTS_PRECOMPUTED) {
+        w = blend_weight(t, dims, v.border, v.range, lut);
+    } else if (weight_type == SPIM_WEIGHTS_VIRTUAL) {
+        const double q0 = double(x + bx), q1 = double(y + by), q2 = double(z + bz);
+        float u[3];
+        for (int r = 0; r < 3; ++r)
+            u[r] = float(q0 * v.a.full[4 * r] + q1 * v.a.full[4 * r + 1] + q2 * v.a.full[4 * r + 2] +
+                         v.a.full[4 * r + 3]);
+        w = blend_weight(u, dims, v.border, v.range, lut);
+    }
+    w_out[i] = w;
+}
+
+// WeightNormalizer: sum over views (double, view order), count of views with w > 0;
+// PRECOMPUTED: w /= sum in place; VIRTUAL: S = sum > 1 ? (float) sum : 1.
+// Overlap statistics per reference portion: atomic min of the count, atomic sum.
+__global__ __launch_bounds__(kIpBlock) void k_weight_sum(float* const* __restrict__ ws, int nviews, int64_t n,
+                                                         int weight_type, float* __restrict__ S,
+                                                         int64_t chunk, int nportions,
+                                                         int* __restrict__ pmin,
+                                                         unsigned long long* __restrict__ psum) {
+    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
+    int cnt = nviews;
+    int port = -1;
+    if (i < n) {
+        double sum = 0.0;
+        cnt = 0;
+        for (int v = 0; v < nviews; ++v) {
+            const float w = ws[v][i];
+            sum += w;
+            if (w > 0.0f) ++cnt;
+        }
+        if (weight_type == SPIM_WEIGHTS_PRECOMPUTED) {
+            for (int v = 0; v < nviews; ++v) ws[v][i] = float(double(ws[v][i]) / sum);
+        } else {
+            S[i] = sum > 1.0 ? float(sum) : 1.0f;
+        }
+        // the last portion takes the remainder (all of it when size < portions)
+        port = chunk > 0 ? int(i / chunk) : nportions - 1;
+        if (port >= nportions) port = nportions - 1;
+    }
+    // one atomic pair per wave when the wave lies in one portion (the common case)
+    const int p0 = __shfl(port, 0, 64);
+    const bool uniform = __all(port == p0 || port < 0);
+    if (uniform && p0 >= 0) {
+        int m = port >= 0 ? cnt : nviews;
+        unsigned long long sm = port >= 0 ? (unsigned long long)cnt : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            m = min(m, __shfl_xor(m, off, 64));
+            sm += __shfl_xor(sm, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&pmin[p0], m);
+            atomicAdd(&psum[p0], sm);
+        }
+    } else if (!uniform && port >= 0) {
+        atomicMin(&pmin[port], cnt);
+        atomicAdd(&psum[port], (unsigned long long)cnt);
+    }
+}
+
+__global__ __launch_bounds__(kIpBlock) void k_final_weight(float* __restrict__ w, const float* __restrict__ S,
+                                                           int64_t n, int weight_type, double osem) {
+    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
+    if (i >= n) return;
+    // Java Math.min propagates NaN (PRECOMPUTED weights are NaN where no view has data)
+    if (weight_type == SPIM_WEIGHTS_VIRTUAL) {
+        const double v = (double(w[i]) / double(S[i])) * osem;
+        w[i] = float(isnan(v) ? v : fmin(1.0, v));
+    } else if (weight_type == SPIM_WEIGHTS_PRECOMPUTED && osem != 1.0) {
+        const float v = w[i] * float(osem);
+        w[i] = isnan(v) ? v : fminf(1.0f, v);
+    }
+}
+
+std::vector<double> blending_lut() {
+    std::vector<double> lut(1001, 0.0);
+    for (double d = 0; d <= 1.0001; d = d + 0.001)
+        lut[size_t(std::floor(d * 1000.0 + 0.5))] = (std::cos((1 - d) * M_PI) + 1) / 2;
+    return lut;
+}
+
+AffineInv invert_model(const double* m) {
+    const double a00 = m[0], a01 = m[1], a02 = m[2], a10 = m[4], a11 = m[5], a12 = m[6];
+    const double a20 = m[8], a21 = m[9], a22 = m[10];
+    const double det = a00 * (a11 * a22 - a12 * a21) - a01 * (a10 * a22 - a12 * a20) +
+                       a02 * (a10 * a21 - a11 * a20);
+    SD_CHECK(det != 0.0 && std::isfinite(det), SPIMDECON_ERR_ARG, "affine model is not invertible");
+    AffineInv r{};
+    r.inv[0] = (a11 * a22 - a12 * a21) / det;
+    r.inv[1] = (a02 * a21 - a01 * a22) / det;
+    r.inv[2] = (a01 * a12 - a02 * a11) / det;
+    r.inv[3] = (a12 * a20 - a10 * a22) / det;
+    r.inv[4] = (a00 * a22 - a02 * a20) / det;
+    r.inv[5] = (a02 * a10 - a00 * a12) / det;
+    r.inv[6] = (a10 * a21 - a11 * a20) / det;
+    r.inv[7] = (a01 * a20 - a00 * a21) / det;
+    r.inv[8] = (a00 * a11 - a01 * a10) / det;
+    r.tr[0] = m[3];
+    r.tr[1] = m[7];
+    r.tr[2] = m[11];
+    for (int row = 0; row < 3; ++row) {
+        for (int c = 0; c < 3; ++c) r.full[4 * row + c] = r.inv[3 * row + c];
+        r.full[4 * row + 3] =
+            -(r.inv[3 * row] * r.tr[0] + r.inv[3 * row + 1] * r.tr[1] + r.inv[3 * row + 2] * r.tr[2]);
+    }
+    return r;
+}
+
+}  // namespace
+
+void prepare_inputs(int nviews, const spim_view_source* views, const spim_input_params* p, float* const* img_out,
+                    float* const* w_out, double* osem_used, int* min_overlap, double* avg_overlap) {
+    SD_CHECK(nviews >= 1 && views && p && img_out && w_out, SPIMDECON_ERR_ARG, "null argument");
+    SD_CHECK(p->weight_type == SPIM_WEIGHTS_NONE || p->weight_type == SPIM_WEIGHTS_PRECOMPUTED ||
+                 p->weight_type == SPIM_WEIGHTS_VIRTUAL,
+             SPIMDECON_ERR_ARG, "unknown weight type");
+    SD_CHECK(p->bb_dims[0] >= 1 && p->bb_dims[1] >= 1 && p->bb_dims[2] >= 1, SPIMDECON_ERR_ARG, "bad bounding box");
+    SD_CHECK(p->ij_threads >= 1, SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
+    check_device(p->device);
+    DeviceGuard guard(p->device);
+    hipStream_t s;
+    SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    struct SG {
+        hipStream_t s;
+        ~SG() { (void)hipStreamDestroy(s); }
+    } sg{s};
+    const int64_t nx = p->bb_dims[0], ny = p->bb_dims[1], nz = p->bb_dims[2];
+    const int64_t n = nx * ny * nz;
+    const unsigned grid = unsigned(ceil_div(n, int64_t(kIpBlock)));
+    const std::vector<double> lut = blending_lut();
+    DBuf<double> dlut(lut.size());
+    SD_HIP(hipMemcpyAsync(dlut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice, s));
+
+    // per-view outputs on the device (the caller's buffers when out_on_device)
+    std::vector<DBuf<float>> own_img(nviews), own_w(nviews);
+    std::vector<float*> dimg(nviews), dw(nviews);
+    for (int v = 0; v < nviews; ++v) {
+        if (p->out_on_device) {
+            dimg[v] = img_out[v];
+            dw[v] = w_out[v];
+        } else {
+            own_img[v].alloc(n);
+            own_w[v].alloc(n);
+            dimg[v] = own_img[v].p;
+            dw[v] = own_w[v].p;
+        }
+    }
+    for (int v = 0; v < nviews; ++v) {
+        const spim_view_source& vs = views[v];
+        SD_CHECK(vs.img && vs.dims[0] >= 1 && vs.dims[1] >= 1 && vs.dims[2] >= 1, SPIMDECON_ERR_ARG,
+                 "bad view source");
+        SD_CHECK(vs.dims[0] < (1 << 30) && vs.dims[1] < (1 << 30) && vs.dims[2] < (1 << 30), SPIMDECON_ERR_ARG,
+                 "view too large");
+        ViewArgs a{};
+        const int64_t sn = vs.dims[0] * vs.dims[1] * vs.dims[2];
+        DBuf<float> dsrc;
+        if (p->src_on_device) {
+            a.src = vs.img;
+        } else {
+            dsrc.alloc(sn);
+            SD_HIP(hipMemcpyAsync(dsrc.p, vs.img, sn * 4, hipMemcpyHostToDevice, s));
+            a.src = dsrc.p;
+        }
+        a.sx = int(vs.dims[0]);
+        a.sy = int(vs.dims[1]);
+        a.sz = int(vs.dims[2]);
+        a.a = invert_model(vs.model);
+        for (int d = 0; d < 3; ++d) {
+            a.border[d] = p->blending_border[d];
+            a.range[d] = p->blending_range[d];
+        }
+        hipLaunchKernelGGL(k_transform_view, dim3(grid), dim3(kIpBlock), 0, s, a, p->bb_min[0], p->bb_min[1],
+                           p->bb_min[2], nx, ny, n, p->weight_type, dlut.p, dimg[v], dw[v]);
+        SD_HIP(hipGetLastError());
+        SD_HIP(hipStreamSynchronize(s));  // the source buffer is released at the end of the iteration
+    }
+    double osem = 1.0;
+    int mn = -1;
+    double av = std::nan("");
+    if (p->weight_type != SPIM_WEIGHTS_NONE) {
+        const int np = 2 * p->ij_threads;  // FusionHelper.divideIntoPortions(size, 2T)
+        DBuf<float*> dws(nviews);
+        SD_HIP(hipMemcpyAsync(dws.p, dw.data(), nviews * sizeof(float*), hipMemcpyHostToDevice, s));
+        DBuf<float> S(p->weight_type == SPIM_WEIGHTS_VIRTUAL ? n : 1);
+        DBuf<int> pmin(np);
+        DBuf<unsigned long long> psum(np);
+        std::vector<int> hmin(np, nviews);
+        SD_HIP(hipMemcpyAsync(pmin.p, hmin.data(), np * 4, hipMemcpyHostToDevice, s));
+        SD_HIP(hipMemsetAsync(psum.p, 0, np * 8, s));
+        hipLaunchKernelGGL(k_weight_sum, dim3(grid), dim3(kIpBlock), 0, s, dws.p, nviews, n, p->weight_type, S.p,
+                           n / np, np, pmin.p, psum.p);
+        SD_HIP(hipGetLastError());
+        std::vector<unsigned long long> hsum(np);
+        SD_HIP(hipMemcpyAsync(hmin.data(), pmin.p, np * 4, hipMemcpyDeviceToHost, s));
+        SD_HIP(hipMemcpyAsync(hsum.data(), psum.p, np * 8, hipMemcpyDeviceToHost, s));
+        SD_HIP(hipStreamSynchronize(s));
+        // WeightNormalizer.process (:74-86): min over portions, mean of per-portion means
+        mn = nviews;
+        double acc = 0.0;
+        for (int q = 0; q < np; ++q) {
+            const int64_t loop = q == np - 1 ? n - (n / np) * (np - 1) : n / np;
+            mn = std::min(mn, hmin[q]);
+            acc += loop > 0 ? double(hsum[q]) / double(loop) : std::nan("");
+        }
+        av = acc / np;
+        // ProcessForDeconvolution.java:318-336
+        osem = p->osem_index == 1 ? double(std::max(1, mn))
+               : p->osem_index == 2 ? std::max(1.0, av)
+                                    : p->osem_speedup;
+        for (int v = 0; v < nviews; ++v)
+            hipLaunchKernelGGL(k_final_weight, dim3(grid), dim3(kIpBlock), 0, s, dw[v], S.p, n, p->weight_type,
+                               osem);
+        SD_HIP(hipGetLastError());
+    }
+    if (!p->out_on_device) {
+        for (int v = 0; v < nviews; ++v) {
+            SD_HIP(hipMemcpyAsync(img_out[v], dimg[v], n * 4, hipMemcpyDeviceToHost, s));
+            SD_HIP(hipMemcpyAsync(w_out[v], dw[v], n * 4, hipMemcpyDeviceToHost, s));
+        }
+    }
+    SD_HIP(hipStreamSynchronize(s));
+    if (osem_used) *osem_used = osem;
+    if (min_overlap) *min_overlap = mn;
+    if (avg_overlap) *avg_overlap = av;
+}
+
+}  // namespace spimdecon
+
+using namespace spimdecon;
+
+extern "C" void spim_input_params_default(spim_input_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    for (int d = 0; d < 3; ++d) {
+        p->blending_border[d] = -8.0f;  // EfficientBayesianBased.java:75-76 (range 12, border -8)
+        p->blending_range[d] = 12.0f;
+    }
+    p->weight_type = SPIM_WEIGHTS_VIRTUAL;
+    p->osem_index = 0;
+    p->osem_speedup = 1.0;
+    p->ij_threads = 8;
+    p->device = 0;
+}
+
+extern "C" int spim_prepare_inputs(int nviews, const spim_view_source* views, const spim_input_params* p,
+                                   float* const* img_out, float* const* weight_out, double* osem_used,
+                                   int* min_overlap, double* avg_overlap) {
+    return guarded([&] {
+        prepare_inputs(nviews, views, p, img_out, weight_out, osem_used, min_overlap, avg_overlap);
+    });
+}

@@ -1,0 +1,65 @@
+"""Host-side mirror of the deconvolution input preparation.
+
+``ProcessForDeconvolution.fuseStacksAndGetPSFs``
+(spim/process/fusion/deconvolution/ProcessForDeconvolution.java:159-384): each
+view is resampled into the fused bounding box through the inverse of its
+affine model, cosine blending weights are computed at the same source
+positions, normalised across views (``WeightNormalizer``) and adjusted for the
+OSEM speed-up -- all on the GPU in ``spim_prepare_inputs``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from enum import IntEnum
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, fptr
+
+
+class WeightType(IntEnum):
+    """ProcessForDeconvolution.WeightType members on the deconvolution path."""
+    NO_WEIGHTS = 0
+    PRECOMPUTED_WEIGHTS = 1
+    VIRTUAL_WEIGHTS = 2
+
+
+def prepare_inputs(srcs, models, bb_min, bb_dims, blending_border=(-8, -8, -8), blending_range=(12, 12, 12),
+                   weight_type: WeightType = WeightType.VIRTUAL_WEIGHTS, osem_index: int = 0,
+                   osem_speedup: float = 1.0, ij_threads: int = 8, device: int = 0):
+    """srcs: [z, y, x] float32 stacks; models: 3x4 (source -> world) affine per
+    view; bb_min / bb_dims: (x, y, z).  Returns (imgs, weights, info) with
+    imgs/weights [z, y, x] float32 per view and info = {osem, min_overlap,
+    avg_overlap}."""
+    lib = _lib.load()
+    V = len(srcs)
+    if V < 1 or len(models) != V:
+        raise ValueError("need one model per view")
+    srcs = [np.ascontiguousarray(s, np.float32) for s in srcs]
+    views = (_lib.ViewSource * V)()
+    for v, (s, m) in enumerate(zip(srcs, models)):
+        if s.ndim != 3:
+            raise ValueError("sources must be 3D [z, y, x]")
+        views[v].img = fptr(s)
+        views[v].dims[:] = [s.shape[2], s.shape[1], s.shape[0]]
+        views[v].model[:] = [float(x) for x in np.asarray(m, np.float64).reshape(12)]
+    p = _lib.InputParams()
+    lib.spim_input_params_default(C.byref(p))
+    p.bb_min[:] = [int(x) for x in bb_min]
+    p.bb_dims[:] = [int(x) for x in bb_dims]
+    p.blending_border[:] = [float(x) for x in blending_border]
+    p.blending_range[:] = [float(x) for x in blending_range]
+    p.weight_type = int(weight_type)
+    p.osem_index = int(osem_index)
+    p.osem_speedup = float(osem_speedup)
+    p.ij_threads = int(ij_threads)
+    p.device = int(device)
+    shape = (int(bb_dims[2]), int(bb_dims[1]), int(bb_dims[0]))
+    imgs = [np.empty(shape, np.float32) for _ in range(V)]
+    ws = [np.empty(shape, np.float32) for _ in range(V)]
+    ip = (_lib._pf * V)(*[fptr(a) for a in imgs])
+    wp = (_lib._pf * V)(*[fptr(a) for a in ws])
+    osem, mn, av = C.c_double(), C.c_int(), C.c_double()
+    check(lib.spim_prepare_inputs(V, views, C.byref(p), ip, wp, C.byref(osem), C.byref(mn), C.byref(av)))
+    return imgs, ws, {"osem": osem.value, "min_overlap": mn.value, "avg_overlap": av.value}

@@ -1,0 +1,59 @@
+"""GPU parity of the deconvolution input preparation against the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import input_ref as ir
+from spim_registration_amd.input_prep import WeightType, prepare_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def rot(axis, deg):
+    c, s = math.cos(math.radians(deg)), math.sin(math.radians(deg))
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def views(V=3, shape=(18, 20, 22), seed=5):
+    rng = np.random.default_rng(seed)
+    srcs, models = [], []
+    for v in range(V):
+        srcs.append((rng.random(shape) * 100 + 1).astype(np.float32))
+        a = rot("y", 360.0 / V * v + 7) @ rot("z", 5 * v) @ np.diag([1.0, 1.0, 1.6])
+        m = np.zeros((3, 4))
+        m[:, :3] = a
+        m[:, 3] = [2.3 + v, -1.7, 3.1 * v]
+        models.append(m)
+    return srcs, models
+
+
+@pytest.mark.parametrize("wt", list(WeightType))
+@pytest.mark.parametrize("osem_index,osem", [(0, 1.0), (0, 2.5), (1, 1.0), (2, 1.0)])
+def test_prepare_inputs_matches_oracle(gpu, wt, osem_index, osem):
+    srcs, models = views()
+    bb_min, bb_dims = (-12, -10, -8), (40, 34, 30)
+    imgs, ws, info = prepare_inputs(srcs, models, bb_min, bb_dims, (-2, -2, -1), (6, 6, 4), wt,
+                                    osem_index, osem)
+    ei, ew, eo = ir.prepare_inputs(srcs, models, bb_min, bb_dims, (-2, -2, -1), (6, 6, 4), int(wt),
+                                   osem_index, osem)
+    for v in range(len(srcs)):
+        bad = np.abs(imgs[v] - ei[v]) > 1e-5 * np.maximum(1, np.abs(ei[v]))
+        assert bad.mean() < 1e-4, (v, bad.sum())           # floor ties may flip a few voxels
+        np.testing.assert_allclose(ws[v], ew[v], rtol=1e-5, atol=1e-6)
+        assert (imgs[v] > 0).any() and (imgs[v] == 0).any()  # bounding box larger than a view
+    if wt != WeightType.NO_WEIGHTS:
+        assert info["osem"] == pytest.approx(eo)
+
+
+def test_identity_model_reproduces_source(gpu):
+    """An identity model over the source's own extent is a copy (>= minValue)."""
+    srcs, _ = views(V=1)
+    ident = np.hstack([np.eye(3), np.zeros((3, 1))])
+    s = srcs[0]
+    imgs, ws, _ = prepare_inputs([s], [ident], (0, 0, 0), (s.shape[2], s.shape[1], s.shape[0]),
+                                 weight_type=WeightType.NO_WEIGHTS)
+    np.testing.assert_array_equal(imgs[0], np.maximum(np.float32(1e-4), s))
+    assert (ws[0] == 1).all()

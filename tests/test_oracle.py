@@ -186,3 +186,29 @@ def test_quadratic_localization_recovers_paraboloid_vertex():
     # flat neighbourhood: singular Hessian -> the peak stays as detected
     flat = np.zeros((5, 5, 5), np.float32)
     assert dog_ref.quadratic_localization(flat, [(2, 2, 2, 0.25)]) == [(2.0, 2.0, 2.0, np.float32(0.25))]
+
+
+def test_input_prep_oracle_rules():
+    """SURVEY 8f #1 restatement: blending table, identity resampling, weight
+    normalisation rules (BlendingRealRandomAccess.java:25-104,
+    WeightNormalizer.java:117-205, NormalizingRandomAccess.java:36-45)."""
+    from oracle import input_ref as ir
+    assert ir.LUT[0] == 0.0 and abs(ir.LUT[1000] - 1.0) < 1e-12 and abs(ir.LUT[500] - 0.5) < 1e-9
+    w = ir.blending_weight(np.array([[0, 5, 5], [10, 5, 5], [5, 5, 5]], np.float32), (11, 11, 11),
+                           (0, 0, 0), (4, 4, 4))
+    assert w[0] == 0 and w[1] == 0 and w[2] == 1
+    rng = np.random.default_rng(3)
+    src = (rng.random((6, 7, 8)) + 0.5).astype(np.float32)
+    ident = np.hstack([np.eye(3), np.zeros((3, 1))])
+    img, _ = ir.transform_view(src, ident, (0, 0, 0), (8, 7, 6), (0, 0, 0), (3, 3, 3), ir.NO_WEIGHTS)
+    np.testing.assert_array_equal(img, src)
+    shifted = ident.copy()
+    shifted[0, 3] = 3.0                                    # view 2 moved 3 voxels in x
+    imgs, ws, _ = ir.prepare_inputs([src, src], [ident, shifted], (0, 0, 0), (11, 7, 6), (0, 0, 0),
+                                    (2, 2, 2), ir.PRECOMPUTED_WEIGHTS)
+    tot = ws[0] + ws[1]
+    covered = np.isfinite(tot)
+    np.testing.assert_allclose(tot[covered], 1.0, rtol=1e-6)
+    imgs, ws, _ = ir.prepare_inputs([src, src], [ident, shifted], (0, 0, 0), (11, 7, 6), (0, 0, 0),
+                                    (2, 2, 2), ir.VIRTUAL_WEIGHTS, osem_index=0, osem=3.0)
+    assert max(float(w.max()) for w in ws) <= 1.0
