@@ -301,6 +301,30 @@ int spim_prepare_inputs(int nviews, const spim_view_source* views, const spim_in
                         float* const* img_out, float* const* weight_out, double* osem_used,
                         int* min_overlap, double* avg_overlap);
 
+/* ======================================================================
+ * 8. Weighted-average fusion --
+ *    spim/process/fusion/weightedavg/ProcessParalellPortion(Weight).java:
+ *    per fused voxel the (blending-weighted) mean of the views covering it.
+ * ====================================================================== */
+typedef struct spim_fusion_params {
+    int64_t bb_min[3];      /* bounding box (world voxels)                               */
+    int64_t bb_dims[3];     /* fused image dims (after downsampling)                    */
+    float   downsampling;   /* 1 = none; s = position * downsampling + bb_min            */
+    int     interpolation;  /* 0 nearest neighbour, 1 n-linear (Fusion.defaultInterpolation) */
+    int     use_blending;   /* Fusion.defaultUseBlending (content-based not supported)  */
+    int     device;
+    int     src_on_device;
+    int     out_on_device;
+    int     reserved[8];
+} spim_fusion_params;
+
+void spim_fusion_params_default(spim_fusion_params* p);
+
+/* blending_borders / blending_ranges: 3 floats per view (may be NULL without
+ * blending); out: bb_dims voxels, x-fastest float32. */
+int spim_fuse_weighted_average(int nviews, const spim_view_source* views, const spim_fusion_params* p,
+                               const float* blending_borders, const float* blending_ranges, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,15 +97,23 @@ def _grid(bb_min, bb_dims):
     return x + int(bb_min[0]), y + int(bb_min[1]), z + int(bb_min[2])
 
 
-def image_positions(model, bb_min, bb_dims) -> np.ndarray:
+def image_positions(model, bb_min, bb_dims, downsampling: float = 1.0) -> np.ndarray:
     """DECON/TransformInput.java:74-95: s = (float) cursor position + offset,
     t = transform.applyInverse(s) (restated: inv3 . (s - translation) in double,
-    rounded to float).  Returns float32 [nz, ny, nx, 3]."""
+    rounded to float).  With ``downsampling`` != 1 (weighted-average fusion,
+    weightedavg/ProcessParalellPortion.java:86-95) s = pos * ds + bb.min in float.
+    Returns float32 [nz, ny, nx, 3]."""
     _, inv, tr = invert_affine(model)
-    gx, gy, gz = _grid(bb_min, bb_dims)
-    s = [g.astype(np.float32).astype(np.float64) for g in (gx, gy, gz)]
+    nx, ny, nz = (int(v) for v in bb_dims)
+    z, y, x = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    s = []
+    for g, b in zip((x, y, z), bb_min):
+        f = g.astype(np.float32)
+        if downsampling != 1.0:
+            f = (f * np.float32(downsampling)).astype(np.float32)
+        s.append((f + np.float32(b)).astype(np.float32).astype(np.float64))
     d = [s[i] - tr[i] for i in range(3)]
-    out = np.empty(gx.shape + (3,), np.float32)
+    out = np.empty(x.shape + (3,), np.float32)
     for r in range(3):
         out[..., r] = (inv[r, 0] * d[0] + inv[r, 1] * d[1] + inv[r, 2] * d[2]).astype(np.float32)
     return out

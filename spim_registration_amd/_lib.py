@@ -74,6 +74,12 @@ class InputParams(C.Structure):
                 ("out_on_device", C.c_int), ("reserved", C.c_int * 8)]
 
 
+class FusionParams(C.Structure):
+    _fields_ = [("bb_min", C.c_int64 * 3), ("bb_dims", C.c_int64 * 3), ("downsampling", C.c_float),
+                ("interpolation", C.c_int), ("use_blending", C.c_int), ("device", C.c_int),
+                ("src_on_device", C.c_int), ("out_on_device", C.c_int), ("reserved", C.c_int * 8)]
+
+
 class InterestPointC(C.Structure):
     _fields_ = [("pos", C.c_double * 3), ("intensity", C.c_float), ("is_max", C.c_int32)]
 
@@ -120,6 +126,9 @@ SIGNATURES = {
     "spim_dog_interest_points": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf,
                                            C.POINTER(InterestPointC), _i64, _pi64]),
     "spim_input_params_default": (None, [C.POINTER(InputParams)]),
+    "spim_fusion_params_default": (None, [C.POINTER(FusionParams)]),
+    "spim_fuse_weighted_average": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(FusionParams),
+                                             _pf, _pf, _pf]),
     "spim_prepare_inputs": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(InputParams),
                                       C.POINTER(_pf), C.POINTER(_pf), C.POINTER(C.c_double),
                                       C.POINTER(C.c_int), C.POINTER(C.c_double)]),

@@ -188,6 +188,63 @@ __global__ __launch_bounds__(kIpBlock) void k_final_weight(float* __restrict__ w
     }
 }
 
+// ---------------------------------------------------------------- weighted-average fusion
+// spim/process/fusion/weightedavg/ProcessParalellPortionWeight.java:86-127 (blending)
+// and ProcessParalellPortion.java:86-120 (plain mean); SURVEY 8f #3.
+struct FuseView {
+    const float* src;
+    int sx, sy, sz;
+    double inv[9], tr[3];
+    float border[3], range[3];
+};
+
+__device__ float nearest1(const float* src, int sx, int sy, int sz, const float t[3]) {
+    const int x = mirror1(int(floor(double(t[0]) + 0.5)), sx);
+    const int y = mirror1(int(floor(double(t[1]) + 0.5)), sy);
+    const int z = mirror1(int(floor(double(t[2]) + 0.5)), sz);
+    return src[(int64_t(z) * sy + y) * sx + x];
+}
+
+__global__ __launch_bounds__(kIpBlock) void k_fuse(const FuseView* __restrict__ views, int nviews, int64_t bx,
+                                                   int64_t by, int64_t bz, int64_t nx, int64_t ny, int64_t n,
+                                                   float ds, int interp, int blend, const double* __restrict__ lut,
+                                                   float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    float f0 = float(x), f1 = float(y), f2 = float(z);
+    if (ds != 1.0f) {
+        f0 = f0 * ds;
+        f1 = f1 * ds;
+        f2 = f2 * ds;
+    }
+    const float s0 = f0 + float(bx), s1 = f1 + float(by), s2 = f2 + float(bz);
+    double sum = 0.0, sumw = 0.0;
+    int cnt = 0;
+    for (int v = 0; v < nviews; ++v) {
+        const FuseView& fv = views[v];
+        const double d0 = double(s0) - fv.tr[0], d1 = double(s1) - fv.tr[1], d2 = double(s2) - fv.tr[2];
+        float t[3];
+        for (int r = 0; r < 3; ++r)
+            t[r] = float(fv.inv[3 * r] * d0 + fv.inv[3 * r + 1] * d1 + fv.inv[3 * r + 2] * d2);
+        if (!(t[0] >= 0.0f && t[1] >= 0.0f && t[2] >= 0.0f && t[0] < float(fv.sx) && t[1] < float(fv.sy) &&
+              t[2] < float(fv.sz)))
+            continue;
+        const double val = interp ? double(nlinear(fv.src, fv.sx, fv.sy, fv.sz, t))
+                                  : double(nearest1(fv.src, fv.sx, fv.sy, fv.sz, t));
+        if (blend) {
+            const int dims[3] = {fv.sx, fv.sy, fv.sz};
+            const double w = blend_weight(t, dims, fv.border, fv.range, lut);
+            sum += val * w;
+            sumw += w;
+        } else {
+            sum += val;
+            ++cnt;
+        }
+    }
+    out[i] = blend ? (sumw > 0.0 ? float(sum / sumw) : 0.0f) : (cnt > 0 ? float(sum / cnt) : 0.0f);
+}
+
 std::vector<double> blending_lut() {
     std::vector<double> lut(1001, 0.0);
     for (double d = 0; d <= 1.0001; d = d + 0.001)
@@ -340,9 +397,85 @@ void prepare_inputs(int nviews, const spim_view_source* views, const spim_input_
     if (avg_overlap) *avg_overlap = av;
 }
 
+void fuse_weighted_average(int nviews, const spim_view_source* views, const spim_fusion_params* p,
+                           const float* borders, const float* ranges, float* out) {
+    SD_CHECK(nviews >= 1 && views && p && out, SPIMDECON_ERR_ARG, "null argument");
+    SD_CHECK(!p->use_blending || (borders && ranges), SPIMDECON_ERR_ARG, "blending needs borders and ranges");
+    SD_CHECK(p->bb_dims[0] >= 1 && p->bb_dims[1] >= 1 && p->bb_dims[2] >= 1, SPIMDECON_ERR_ARG, "bad bounding box");
+    SD_CHECK(p->interpolation == 0 || p->interpolation == 1, SPIMDECON_ERR_ARG, "interpolation must be 0 or 1");
+    check_device(p->device);
+    DeviceGuard guard(p->device);
+    hipStream_t s;
+    SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    struct SG {
+        hipStream_t s;
+        ~SG() { (void)hipStreamDestroy(s); }
+    } sg{s};
+    const int64_t nx = p->bb_dims[0], ny = p->bb_dims[1], nz = p->bb_dims[2];
+    const int64_t n = nx * ny * nz;
+    const std::vector<double> lut = blending_lut();
+    DBuf<double> dlut(lut.size());
+    SD_HIP(hipMemcpyAsync(dlut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice, s));
+    std::vector<DBuf<float>> srcs(nviews);
+    std::vector<FuseView> fv(nviews);
+    for (int v = 0; v < nviews; ++v) {
+        const spim_view_source& vs = views[v];
+        SD_CHECK(vs.img && vs.dims[0] >= 1 && vs.dims[1] >= 1 && vs.dims[2] >= 1 && vs.dims[0] < (1 << 30) &&
+                     vs.dims[1] < (1 << 30) && vs.dims[2] < (1 << 30),
+                 SPIMDECON_ERR_ARG, "bad view source");
+        const int64_t sn = vs.dims[0] * vs.dims[1] * vs.dims[2];
+        if (p->src_on_device) {
+            fv[v].src = vs.img;
+        } else {
+            srcs[v].alloc(sn);
+            SD_HIP(hipMemcpyAsync(srcs[v].p, vs.img, sn * 4, hipMemcpyHostToDevice, s));
+            fv[v].src = srcs[v].p;
+        }
+        fv[v].sx = int(vs.dims[0]);
+        fv[v].sy = int(vs.dims[1]);
+        fv[v].sz = int(vs.dims[2]);
+        const AffineInv a = invert_model(vs.model);
+        std::memcpy(fv[v].inv, a.inv, sizeof(a.inv));
+        std::memcpy(fv[v].tr, a.tr, sizeof(a.tr));
+        for (int d = 0; d < 3; ++d) {
+            fv[v].border[d] = borders ? borders[3 * v + d] : 0.0f;
+            fv[v].range[d] = ranges ? ranges[3 * v + d] : 1.0f;
+        }
+    }
+    DBuf<FuseView> dfv(nviews);
+    SD_HIP(hipMemcpyAsync(dfv.p, fv.data(), nviews * sizeof(FuseView), hipMemcpyHostToDevice, s));
+    DBuf<float> dout;
+    float* o = out;
+    if (!p->out_on_device) {
+        dout.alloc(n);
+        o = dout.p;
+    }
+    hipLaunchKernelGGL(k_fuse, dim3(unsigned(ceil_div(n, int64_t(kIpBlock)))), dim3(kIpBlock), 0, s, dfv.p,
+                       nviews, p->bb_min[0], p->bb_min[1], p->bb_min[2], nx, ny, n, p->downsampling,
+                       p->interpolation, p->use_blending ? 1 : 0, dlut.p, o);
+    SD_HIP(hipGetLastError());
+    if (!p->out_on_device) SD_HIP(hipMemcpyAsync(out, o, n * 4, hipMemcpyDeviceToHost, s));
+    SD_HIP(hipStreamSynchronize(s));
+}
+
 }  // namespace spimdecon
 
 using namespace spimdecon;
+
+extern "C" void spim_fusion_params_default(spim_fusion_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->downsampling = 1.0f;
+    p->interpolation = 1;  // Fusion.defaultInterpolation (linear)
+    p->use_blending = 1;   // Fusion.defaultUseBlending
+    p->device = 0;
+}
+
+extern "C" int spim_fuse_weighted_average(int nviews, const spim_view_source* views, const spim_fusion_params* p,
+                                          const float* blending_borders, const float* blending_ranges,
+                                          float* out) {
+    return guarded([&] { fuse_weighted_average(nviews, views, p, blending_borders, blending_ranges, out); });
+}
 
 extern "C" void spim_input_params_default(spim_input_params* p) {
     if (!p) return;

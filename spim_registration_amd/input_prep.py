@@ -63,3 +63,34 @@ def prepare_inputs(srcs, models, bb_min, bb_dims, blending_border=(-8, -8, -8), 
     osem, mn, av = C.c_double(), C.c_int(), C.c_double()
     check(lib.spim_prepare_inputs(V, views, C.byref(p), ip, wp, C.byref(osem), C.byref(mn), C.byref(av)))
     return imgs, ws, {"osem": osem.value, "min_overlap": mn.value, "avg_overlap": av.value}
+
+
+def fuse_weighted_average(srcs, models, bb_min, bb_dims, downsampling: float = 1.0, interpolation: int = 1,
+                          use_blending: bool = True, blending_borders=None, blending_ranges=None,
+                          device: int = 0) -> np.ndarray:
+    """Weighted-average fusion (spim/process/fusion/weightedavg/ProcessParalell*.java):
+    [z, y, x] float32 fused volume.  blending_borders / ranges: (x, y, z) per view."""
+    lib = _lib.load()
+    V = len(srcs)
+    srcs = [np.ascontiguousarray(s, np.float32) for s in srcs]
+    views = (_lib.ViewSource * V)()
+    for v, (s, m) in enumerate(zip(srcs, models)):
+        views[v].img = fptr(s)
+        views[v].dims[:] = [s.shape[2], s.shape[1], s.shape[0]]
+        views[v].model[:] = [float(x) for x in np.asarray(m, np.float64).reshape(12)]
+    p = _lib.FusionParams()
+    lib.spim_fusion_params_default(C.byref(p))
+    p.bb_min[:] = [int(x) for x in bb_min]
+    p.bb_dims[:] = [int(x) for x in bb_dims]
+    p.downsampling = float(downsampling)
+    p.interpolation = int(interpolation)
+    p.use_blending = int(bool(use_blending))
+    p.device = int(device)
+    b = r = None
+    if use_blending:
+        b = np.ascontiguousarray(np.asarray(blending_borders, np.float32).reshape(V, 3))
+        r = np.ascontiguousarray(np.asarray(blending_ranges, np.float32).reshape(V, 3))
+    out = np.empty((int(bb_dims[2]), int(bb_dims[1]), int(bb_dims[0])), np.float32)
+    check(lib.spim_fuse_weighted_average(V, views, C.byref(p), fptr(b) if b is not None else None,
+                                         fptr(r) if r is not None else None, fptr(out)))
+    return out

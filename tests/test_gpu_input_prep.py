@@ -5,7 +5,8 @@ import numpy as np
 import pytest
 
 from oracle import input_ref as ir
-from spim_registration_amd.input_prep import WeightType, prepare_inputs
+from oracle import fusion_ref as fr
+from spim_registration_amd.input_prep import WeightType, fuse_weighted_average, prepare_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -57,3 +58,17 @@ def test_identity_model_reproduces_source(gpu):
                                  weight_type=WeightType.NO_WEIGHTS)
     np.testing.assert_array_equal(imgs[0], np.maximum(np.float32(1e-4), s))
     assert (ws[0] == 1).all()
+
+
+@pytest.mark.parametrize("interp,blend,ds", [(1, True, 1.0), (0, True, 1.0), (1, False, 1.0), (1, True, 2.0),
+                                             (0, False, 1.5)])
+def test_weighted_average_fusion_matches_oracle(gpu, interp, blend, ds):
+    """SURVEY 8f #3 (BASELINE configs[0] plumbing): weighted-average fusion."""
+    srcs, models = views(V=2)
+    bb_min, bb_dims = (-10, -9, -8), (36, 30, 26)
+    borders, ranges = [(0, 0, 0), (1, 1, 0)], [(5, 5, 3), (4, 6, 3)]
+    got = fuse_weighted_average(srcs, models, bb_min, bb_dims, ds, interp, blend, borders, ranges)
+    want = fr.fuse_weighted_average(srcs, models, bb_min, bb_dims, ds, interp, blend, borders, ranges)
+    bad = np.abs(got - want) > 1e-5 * np.maximum(1, np.abs(want))
+    assert bad.mean() < 1e-3, bad.sum()                      # nearest/floor ties may flip a few voxels
+    assert (want > 0).any() and (want == 0).any()
