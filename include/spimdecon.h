@@ -325,6 +325,44 @@ void spim_fusion_params_default(spim_fusion_params* p);
 int spim_fuse_weighted_average(int nviews, const spim_view_source* views, const spim_fusion_params* p,
                                const float* blending_borders, const float* blending_ranges, float* out);
 
+/* ======================================================================
+ * 9. PSF extraction / transformation --
+ *    spim/process/fusion/deconvolution/ExtractPSF.java.  All buffers are
+ *    x-fastest float32 in host memory unless stated; dims are (x, y, z).
+ * ====================================================================== */
+
+/* transformPSF (:309-346): odd size of the transformed PSF and the offset that
+ * keeps model(dim / 2) at its centre voxel (offset may be NULL). */
+int spim_psf_transformed_size(const int64_t psf_size[3], const double model[12], int64_t out_size[3],
+                              double offset[3]);
+
+/* transformPSF + transform (:309-346, :424-460): n-linear over a zero-extended
+ * PSF at inverse(model)(i + offset); out holds spim_psf_transformed_size voxels.
+ * Also the path of loadAndTransformPSFs (:520-575) for PSFs read from files. */
+int spim_transform_psf(const float* psf, const int64_t psf_size[3], const double model[12], float* out,
+                       int device);
+
+/* extractNextImg (:260-279): extractPSFLocal (:383-422; the sum over beads of
+ * the n-linear samples of the periodic-extended view at i - size/2 + bead,
+ * locations = nlocations x (x, y, z) local pixel coordinates), normalize
+ * (:281-299) into psf_original (psf_size voxels), then -- when psf_transformed
+ * is not NULL -- transformPSF with the view model.  img may be a device
+ * pointer (img_on_device = 1), e.g. the source stack of spim_prepare_inputs. */
+int spim_extract_psf(const float* img, const int64_t dims[3], int img_on_device, const double* locations,
+                     int64_t nlocations, const int64_t psf_size[3], const double model[12], float* psf_original,
+                     float* psf_transformed, int device);
+
+/* computeAverageTransformedPSF (:164-208): the PSFs (psf_dims = npsfs x 3)
+ * point-mirrored about their centres and summed into the max size, written
+ * to avg_dims.  avg == NULL: only the dims are returned. */
+int spim_average_transformed_psf(int npsfs, const float* const* psfs, const int64_t* psf_dims, float* avg,
+                                 int64_t avg_dims[3], int device);
+
+/* computeMaxProjection (:110-162): max along min_dim (0 x, 1 y, 2 z; < 0 = the
+ * first smallest dimension, returned in used_dim).  out == NULL: dims only. */
+int spim_max_projection(const float* img, const int64_t dims[3], int min_dim, float* out, int64_t out_dims[2],
+                        int* used_dim, int device);
+
 #ifdef __cplusplus
 }
 #endif

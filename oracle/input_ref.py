@@ -141,9 +141,11 @@ def _mirror(i, n):
     return np.where(j >= n, p - j, j)
 
 
-def nlinear(img: np.ndarray, pos: np.ndarray) -> np.ndarray:
-    """NLinearInterpolator3D on FloatType over extendMirrorSingle (PARITY UNPINNED,
-    see the module docstring).  img [nz, ny, nx], pos float32 [..., 3] (x, y, z)."""
+def nlinear(img: np.ndarray, pos: np.ndarray, boundary: str = "mirror") -> np.ndarray:
+    """NLinearInterpolator3D on FloatType (PARITY UNPINNED, see the module
+    docstring) over extendMirrorSingle ("mirror"), extendPeriodic ("periodic")
+    or extendZero ("zero").  img [nz, ny, nx], pos [..., 3] (x, y, z), float32
+    or float64 positions."""
     img = np.asarray(img, np.float32)
     nz, ny, nx = img.shape
     p = pos.astype(np.float64)
@@ -153,7 +155,14 @@ def nlinear(img: np.ndarray, pos: np.ndarray) -> np.ndarray:
     x0, y0, z0 = f[..., 0], f[..., 1], f[..., 2]
 
     def at(dx, dy, dz):
-        return img[_mirror(z0 + dz, nz), _mirror(y0 + dy, ny), _mirror(x0 + dx, nx)]
+        x, y, z = x0 + dx, y0 + dy, z0 + dz
+        if boundary == "mirror":
+            return img[_mirror(z, nz), _mirror(y, ny), _mirror(x, nx)]
+        if boundary == "periodic":
+            return img[np.mod(z, nz), np.mod(y, ny), np.mod(x, nx)]
+        inside = (x >= 0) & (x < nx) & (y >= 0) & (y < ny) & (z >= 0) & (z < nz)
+        v = img[np.clip(z, 0, nz - 1), np.clip(y, 0, ny - 1), np.clip(x, 0, nx - 1)]
+        return np.where(inside, v, np.float32(0))
 
     wt = {(0, 0, 0): wi[..., 0] * wi[..., 1] * wi[..., 2], (1, 0, 0): w[..., 0] * wi[..., 1] * wi[..., 2],
           (0, 1, 0): wi[..., 0] * w[..., 1] * wi[..., 2], (1, 1, 0): w[..., 0] * w[..., 1] * wi[..., 2],

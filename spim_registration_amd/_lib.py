@@ -127,6 +127,11 @@ SIGNATURES = {
                                            C.POINTER(InterestPointC), _i64, _pi64]),
     "spim_input_params_default": (None, [C.POINTER(InputParams)]),
     "spim_fusion_params_default": (None, [C.POINTER(FusionParams)]),
+    "spim_psf_transformed_size": (C.c_int, [_pi64, _pd, _pi64, _pd]),
+    "spim_transform_psf": (C.c_int, [_pf, _pi64, _pd, _pf, C.c_int]),
+    "spim_extract_psf": (C.c_int, [C.c_void_p, _pi64, C.c_int, _pd, C.c_int64, _pi64, _pd, _pf, _pf, C.c_int]),
+    "spim_average_transformed_psf": (C.c_int, [C.c_int, C.POINTER(_pf), _pi64, _pf, _pi64, C.c_int]),
+    "spim_max_projection": (C.c_int, [_pf, _pi64, C.c_int, _pf, _pi64, C.POINTER(C.c_int), C.c_int]),
     "spim_fuse_weighted_average": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(FusionParams),
                                              _pf, _pf, _pf]),
     "spim_prepare_inputs": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(InputParams),
@@ -146,7 +151,13 @@ class SpimDeconError(RuntimeError):
 
 
 def load():
-    """Loads the in-tree library (raises if it has not been built)."""
+    """Loads the in-tree library (raises if it has not been built).
+
+    torch wheels bundle their own libamdhip64.so.7; the loader keeps whichever
+    copy of that soname comes first.  A process that uses torch on the GPU
+    together with this library must import torch before the first load() (as
+    bench.py and tests/test_gpu_psf.py do) so both share torch's HIP runtime;
+    the reverse order hands torch the /opt/rocm runtime and aborts at exit."""
     global _lib
     if _lib is not None:
         return _lib

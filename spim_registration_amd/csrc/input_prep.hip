@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "resample.hpp"
 #include "spimdecon.h"
 
 namespace spimdecon {
@@ -28,26 +29,12 @@ namespace {
 
 constexpr int kIpBlock = 256;
 
-struct AffineInv {
-    double inv[9];   // inverse of the 3x3 part, row-major
-    double tr[3];    // translation of the model
-    double full[12]; // full inverse, row-major 3x4
-};
-
 struct ViewArgs {
     const float* src;
     int sx, sy, sz;
     AffineInv a;
     float border[3], range[3];
 };
-
-__device__ __forceinline__ int mirror1(int i, int n) {
-    if (n == 1) return 0;
-    const int p = 2 * (n - 1);
-    int j = i % p;
-    if (j < 0) j += p;
-    return j >= n ? p - j : j;
-}
 
 // BlendingRealRandomAccess.computeWeight (:78-104), float arithmetic
 __device__ float blend_weight(const float t[3], const int dims[3], const float* border, const float* range,
@@ -69,27 +56,8 @@ __device__ float blend_weight(const float t[3], const int dims[3], const float* 
     return w;
 }
 
-// NLinearInterpolator3D on FloatType over extendMirrorSingle (restated, unpinned)
-__device__ float nlinear(const float* src, int sx, int sy, int sz, const float t[3]) {
-    const double p0 = t[0], p1 = t[1], p2 = t[2];
-    const double f0 = floor(p0), f1 = floor(p1), f2 = floor(p2);
-    const int x0 = int(f0), y0 = int(f1), z0 = int(f2);
-    const double w0 = p0 - f0, w1 = p1 - f1, w2 = p2 - f2;
-    const double i0 = 1.0 - w0, i1 = 1.0 - w1, i2 = 1.0 - w2;
-    const int xa = mirror1(x0, sx), xb = mirror1(x0 + 1, sx);
-    const int ya = mirror1(y0, sy), yb = mirror1(y0 + 1, sy);
-    const int za = mirror1(z0, sz), zb = mirror1(z0 + 1, sz);
-    auto at = [&](int x, int y, int z) { return src[(int64_t(z) * sy + y) * sx + x]; };
-    // corner order 000, 100, 110, 010, 011, 111, 101, 001
-    float acc = float(double(at(xa, ya, za)) * (i0 * i1 * i2));
-    acc = acc + float(double(at(xb, ya, za)) * (w0 * i1 * i2));
-    acc = acc + float(double(at(xb, yb, za)) * (w0 * w1 * i2));
-    acc = acc + float(double(at(xa, yb, za)) * (i0 * w1 * i2));
-    acc = acc + float(double(at(xa, yb, zb)) * (i0 * w1 * w2));
-    acc = acc + float(double(at(xb, yb, zb)) * (w0 * w1 * w2));
-    acc = acc + float(double(at(xb, ya, zb)) * (w0 * i1 * w2));
-    acc = acc + float(double(at(xa, ya, zb)) * (i0 * i1 * w2));
-    return acc;
+__device__ __forceinline__ float nlinear(const float* src, int sx, int sy, int sz, const float t[3]) {
+    return nlinear_at<kExtMirror>(src, sx, sy, sz, t[0], t[1], t[2]);
 }
 
 __global__ __launch_bounds__(kIpBlock) void k_transform_view(ViewArgs v, int64_t bx, int64_t by, int64_t bz,
@@ -250,33 +218,6 @@ std::vector<double> blending_lut() {
     for (double d = 0; d <= 1.0001; d = d + 0.001)
         lut[size_t(std::floor(d * 1000.0 + 0.5))] = (std::cos((1 - d) * M_PI) + 1) / 2;
     return lut;
-}
-
-AffineInv invert_model(const double* m) {
-    const double a00 = m[0], a01 = m[1], a02 = m[2], a10 = m[4], a11 = m[5], a12 = m[6];
-    const double a20 = m[8], a21 = m[9], a22 = m[10];
-    const double det = a00 * (a11 * a22 - a12 * a21) - a01 * (a10 * a22 - a12 * a20) +
-                       a02 * (a10 * a21 - a11 * a20);
-    SD_CHECK(det != 0.0 && std::isfinite(det), SPIMDECON_ERR_ARG, "affine model is not invertible");
-    AffineInv r{};
-    r.inv[0] = (a11 * a22 - a12 * a21) / det;
-    r.inv[1] = (a02 * a21 - a01 * a22) / det;
-    r.inv[2] = (a01 * a12 - a02 * a11) / det;
-    r.inv[3] = (a12 * a20 - a10 * a22) / det;
-    r.inv[4] = (a00 * a22 - a02 * a20) / det;
-    r.inv[5] = (a02 * a10 - a00 * a12) / det;
-    r.inv[6] = (a10 * a21 - a11 * a20) / det;
-    r.inv[7] = (a01 * a20 - a00 * a21) / det;
-    r.inv[8] = (a00 * a11 - a01 * a10) / det;
-    r.tr[0] = m[3];
-    r.tr[1] = m[7];
-    r.tr[2] = m[11];
-    for (int row = 0; row < 3; ++row) {
-        for (int c = 0; c < 3; ++c) r.full[4 * row + c] = r.inv[3 * row + c];
-        r.full[4 * row + 3] =
-            -(r.inv[3 * row] * r.tr[0] + r.inv[3 * row + 1] * r.tr[1] + r.inv[3 * row + 2] * r.tr[2]);
-    }
-    return r;
 }
 
 }  // namespace

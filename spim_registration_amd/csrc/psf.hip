@@ -1,0 +1,354 @@
+// psf.hip -- PSF extraction and transformation on the GPU.
+//
+// Restates spim/process/fusion/deconvolution/ExtractPSF.java (paths under
+// /root/reference/src/main/java/):
+//   extractPSFLocal              :383-422  (n-linear over extendPeriodic, summed per bead)
+//   normalize                    :281-299  ((v - min) / (max - min) in double)
+//   transformPSF + transform     :309-346, :424-460 (odd size, centre kept, extendZero)
+//   computeAverageTransformedPSF :164-208  (point-mirrored sum into the max size)
+//   computeMaxProjection         :110-162
+// One thread per output voxel; PSFs are small (10^4-10^6 voxels), the source
+// stack is read through L2 by the bead loop.  The oracle is oracle/psf_ref.py.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+#include "resample.hpp"
+#include "spimdecon.h"
+
+namespace spimdecon {
+
+namespace {
+
+constexpr int kPsfBlock = 256;
+
+struct Dim3 {
+    int x, y, z;
+    __host__ __device__ int64_t n() const { return int64_t(x) * y * z; }
+};
+
+__global__ __launch_bounds__(kPsfBlock) void k_psf_extract(const float* __restrict__ img, Dim3 s,
+                                                           const double* __restrict__ locs, int64_t nloc, Dim3 p,
+                                                           float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
+    if (i >= p.n()) return;
+    const int x = int(i % p.x), y = int((i / p.x) % p.y), z = int(i / (int64_t(p.x) * p.y));
+    const double r0 = double(x - p.x / 2), r1 = double(y - p.y / 2), r2 = double(z - p.z / 2);
+    float acc = 0.0f;
+    for (int64_t l = 0; l < nloc; ++l)
+        acc = acc + nlinear_at<kExtPeriodic>(img, s.x, s.y, s.z, r0 + locs[3 * l], r1 + locs[3 * l + 1],
+                                             r2 + locs[3 * l + 2]);
+    out[i] = acc;
+}
+
+// single-block min/max (the PSF is small); NaN never wins a comparison, as in Java
+__global__ __launch_bounds__(1024) void k_psf_minmax(const float* __restrict__ v, int64_t n,
+                                                     double* __restrict__ mm) {
+    __shared__ double smin[1024], smax[1024];
+    double lo = DBL_MAX, hi = -DBL_MAX;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) {
+        const double a = v[i];
+        if (a < lo) lo = a;
+        if (a > hi) hi = a;
+    }
+    smin[threadIdx.x] = lo;
+    smax[threadIdx.x] = hi;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if (int(threadIdx.x) < w) {
+            smin[threadIdx.x] = fmin(smin[threadIdx.x], smin[threadIdx.x + w]);
+            smax[threadIdx.x] = fmax(smax[threadIdx.x], smax[threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        mm[0] = smin[0];
+        mm[1] = smax[0];
+    }
+}
+
+__global__ __launch_bounds__(kPsfBlock) void k_psf_normalize(float* __restrict__ v, int64_t n,
+                                                             const double* __restrict__ mm) {
+    const int64_t i = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
+    if (i >= n) return;
+    v[i] = float((double(v[i]) - mm[0]) / (mm[1] - mm[0]));
+}
+
+struct Inv12 {
+    double m[12];
+};
+
+__global__ __launch_bounds__(kPsfBlock) void k_psf_transform(const float* __restrict__ psf, Dim3 s, Inv12 f,
+                                                             double o0, double o1, double o2, Dim3 t,
+                                                             float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
+    if (i >= t.n()) return;
+    const int x = int(i % t.x), y = int((i / t.x) % t.y), z = int(i / (int64_t(t.x) * t.y));
+    const double a = x + o0, b = y + o1, c = z + o2;
+    const double q0 = a * f.m[0] + b * f.m[1] + c * f.m[2] + f.m[3];
+    const double q1 = a * f.m[4] + b * f.m[5] + c * f.m[6] + f.m[7];
+    const double q2 = a * f.m[8] + b * f.m[9] + c * f.m[10] + f.m[11];
+    out[i] = nlinear_at<kExtZero>(psf, s.x, s.y, s.z, q0, q1, q2);
+}
+
+struct PsfRef {
+    const float* p;
+    Dim3 d;
+};
+
+__global__ __launch_bounds__(kPsfBlock) void k_psf_average(const PsfRef* __restrict__ psfs, int npsf, Dim3 m,
+                                                           float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
+    if (i >= m.n()) return;
+    const int x = int(i % m.x), y = int((i / m.x) % m.y), z = int(i / (int64_t(m.x) * m.y));
+    float acc = 0.0f;
+    for (int k = 0; k < npsf; ++k) {
+        const Dim3 d = psfs[k].d;
+        // avg(psfCenter - loc + avgCenter) += psf(loc)
+        const int lx = d.x / 2 + m.x / 2 - x, ly = d.y / 2 + m.y / 2 - y, lz = d.z / 2 + m.z / 2 - z;
+        if (lx < 0 || ly < 0 || lz < 0 || lx >= d.x || ly >= d.y || lz >= d.z) continue;
+        acc = acc + psfs[k].p[(int64_t(lz) * d.y + ly) * d.x + lx];
+    }
+    out[i] = acc;
+}
+
+__global__ __launch_bounds__(kPsfBlock) void k_max_projection(const float* __restrict__ img, Dim3 s, int dim,
+                                                              float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
+    const int n0 = dim == 0 ? s.y : s.x, n1 = dim == 2 ? s.y : s.z;
+    if (i >= int64_t(n0) * n1) return;
+    const int a = int(i % n0), b = int(i / n0);
+    int x, y, z, len;
+    int64_t stride;
+    if (dim == 0) { x = 0; y = a; z = b; len = s.x; stride = 1; }
+    else if (dim == 1) { x = a; y = 0; z = b; len = s.y; stride = s.x; }
+    else { x = a; y = b; z = 0; len = s.z; stride = int64_t(s.x) * s.y; }
+    const float* q = img + (int64_t(z) * s.y + y) * s.x + x;
+    double mx = -DBL_MAX;
+    for (int k = 0; k < len; ++k) {
+        const double v = q[k * stride];
+        if (v > mx) mx = v;
+    }
+    out[i] = float(mx);
+}
+
+Dim3 dim3_of(const int64_t* d, const char* what) {
+    SD_CHECK(d, SPIMDECON_ERR_ARG, std::string(what) + ": null dims");
+    for (int k = 0; k < 3; ++k)
+        SD_CHECK(d[k] >= 1 && d[k] < (int64_t(1) << 30), SPIMDECON_ERR_ARG, std::string(what) + ": bad dims");
+    return Dim3{int(d[0]), int(d[1]), int(d[2])};
+}
+
+unsigned grid_for(int64_t n) { return unsigned(ceil_div(n, int64_t(kPsfBlock))); }
+
+struct Stream {
+    hipStream_t s{};
+    Stream() { SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+    ~Stream() { (void)hipStreamDestroy(s); }
+};
+
+// transformPSF (:309-346): odd size that holds the transformed box, and the
+// offset keeping model(dim / 2) at the centre voxel
+void transformed_size(const int64_t size[3], const double* m, int64_t out[3], double off[3]) {
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int c = 0; c < 8; ++c) {
+        const double p[3] = {(c & 1) ? double(size[0] - 1) : 0.0, (c & 2) ? double(size[1] - 1) : 0.0,
+                             (c & 4) ? double(size[2] - 1) : 0.0};
+        for (int r = 0; r < 3; ++r) {
+            const double t = p[0] * m[4 * r] + p[1] * m[4 * r + 1] + p[2] * m[4 * r + 2] + m[4 * r + 3];
+            lo[r] = std::min(lo[r], t);
+            hi[r] = std::max(hi[r], t);
+        }
+    }
+    const double c[3] = {double(size[0] / 2), double(size[1] / 2), double(size[2] / 2)};
+    for (int r = 0; r < 3; ++r) {
+        int64_t n = int64_t(hi[r] - lo[r]) + 1;
+        if (n % 2 == 0) ++n;
+        out[r] = n;
+        const double t = c[0] * m[4 * r] + c[1] * m[4 * r + 1] + c[2] * m[4 * r + 2] + m[4 * r + 3];
+        off[r] = t - double(n / 2);
+    }
+}
+
+void launch_transform(const float* dpsf, Dim3 s, const double* model, float* dout, Dim3& t, hipStream_t st) {
+    int64_t size[3] = {s.x, s.y, s.z}, ts[3];
+    double off[3];
+    transformed_size(size, model, ts, off);
+    t = dim3_of(ts, "transformed psf");
+    const AffineInv a = invert_model(model);
+    Inv12 f;
+    std::memcpy(f.m, a.full, sizeof(f.m));
+    hipLaunchKernelGGL(k_psf_transform, dim3(grid_for(t.n())), dim3(kPsfBlock), 0, st, dpsf, s, f, off[0], off[1],
+                       off[2], t, dout);
+    SD_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+void psf_transformed_size(const int64_t* psf_size, const double* model, int64_t* out_size, double* offset) {
+    SD_CHECK(model && out_size, SPIMDECON_ERR_ARG, "null argument");
+    dim3_of(psf_size, "psf");
+    double off[3];
+    transformed_size(psf_size, model, out_size, off);
+    (void)invert_model(model);
+    if (offset) std::memcpy(offset, off, sizeof(off));
+}
+
+void transform_psf(const float* psf, const int64_t* psf_size, const double* model, float* out, int device) {
+    SD_CHECK(psf && model && out, SPIMDECON_ERR_ARG, "null argument");
+    const Dim3 s = dim3_of(psf_size, "psf");
+    check_device(device);
+    DeviceGuard guard(device);
+    Stream st;
+    DBuf<float> dp(s.n());
+    SD_HIP(hipMemcpyAsync(dp.p, psf, s.n() * 4, hipMemcpyHostToDevice, st.s));
+    int64_t ts[3];
+    double off[3];
+    transformed_size(psf_size, model, ts, off);
+    DBuf<float> dt(dim3_of(ts, "transformed psf").n());
+    Dim3 t;
+    launch_transform(dp.p, s, model, dt.p, t, st.s);
+    SD_HIP(hipMemcpyAsync(out, dt.p, t.n() * 4, hipMemcpyDeviceToHost, st.s));
+    SD_HIP(hipStreamSynchronize(st.s));
+}
+
+void extract_psf(const float* img, const int64_t* dims, int img_on_device, const double* locations, int64_t nloc,
+                 const int64_t* psf_size, const double* model, float* psf_original, float* psf_transformed,
+                 int device) {
+    SD_CHECK(img && psf_original && nloc >= 0 && (nloc == 0 || locations), SPIMDECON_ERR_ARG, "null argument");
+    SD_CHECK(!psf_transformed || model, SPIMDECON_ERR_ARG, "a transformed PSF needs the view model");
+    const Dim3 s = dim3_of(dims, "image");
+    const Dim3 p = dim3_of(psf_size, "psf");
+    check_device(device);
+    DeviceGuard guard(device);
+    Stream st;
+    DBuf<float> dimg;
+    const float* src = img;
+    if (!img_on_device) {
+        dimg.alloc(s.n());
+        SD_HIP(hipMemcpyAsync(dimg.p, img, s.n() * 4, hipMemcpyHostToDevice, st.s));
+        src = dimg.p;
+    }
+    DBuf<double> dloc(size_t(std::max<int64_t>(nloc, 1)) * 3);
+    if (nloc) SD_HIP(hipMemcpyAsync(dloc.p, locations, nloc * 24, hipMemcpyHostToDevice, st.s));
+    DBuf<float> dpsf(p.n());
+    DBuf<double> mm(2);
+    hipLaunchKernelGGL(k_psf_extract, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, src, s, dloc.p, nloc, p,
+                       dpsf.p);
+    SD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_psf_minmax, dim3(1), dim3(1024), 0, st.s, dpsf.p, p.n(), mm.p);
+    SD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, dpsf.p, p.n(), mm.p);
+    SD_HIP(hipGetLastError());
+    SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDeviceToHost, st.s));
+    DBuf<float> dt;
+    if (psf_transformed) {
+        int64_t ts[3];
+        double off[3];
+        transformed_size(psf_size, model, ts, off);
+        dt.alloc(dim3_of(ts, "transformed psf").n());
+        Dim3 t;
+        launch_transform(dpsf.p, p, model, dt.p, t, st.s);
+        SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, t.n() * 4, hipMemcpyDeviceToHost, st.s));
+    }
+    SD_HIP(hipStreamSynchronize(st.s));
+}
+
+void average_transformed_psf(int npsf, const float* const* psfs, const int64_t* psf_dims, float* avg,
+                             int64_t* avg_dims, int device) {
+    SD_CHECK(npsf >= 1 && psfs && psf_dims && avg_dims, SPIMDECON_ERR_ARG, "null argument");
+    std::vector<Dim3> d(npsf);
+    int64_t m[3] = {0, 0, 0};
+    for (int k = 0; k < npsf; ++k) {
+        d[k] = dim3_of(psf_dims + 3 * k, "psf");
+        m[0] = std::max<int64_t>(m[0], d[k].x);
+        m[1] = std::max<int64_t>(m[1], d[k].y);
+        m[2] = std::max<int64_t>(m[2], d[k].z);
+    }
+    std::memcpy(avg_dims, m, sizeof(m));
+    if (!avg) return;
+    const Dim3 md = dim3_of(m, "average psf");
+    check_device(device);
+    DeviceGuard guard(device);
+    Stream st;
+    std::vector<DBuf<float>> dp(npsf);
+    std::vector<PsfRef> refs(npsf);
+    for (int k = 0; k < npsf; ++k) {
+        SD_CHECK(psfs[k], SPIMDECON_ERR_ARG, "null psf");
+        dp[k].alloc(d[k].n());
+        SD_HIP(hipMemcpyAsync(dp[k].p, psfs[k], d[k].n() * 4, hipMemcpyHostToDevice, st.s));
+        refs[k] = PsfRef{dp[k].p, d[k]};
+    }
+    DBuf<PsfRef> drefs(npsf);
+    SD_HIP(hipMemcpyAsync(drefs.p, refs.data(), npsf * sizeof(PsfRef), hipMemcpyHostToDevice, st.s));
+    DBuf<float> dout(md.n());
+    hipLaunchKernelGGL(k_psf_average, dim3(grid_for(md.n())), dim3(kPsfBlock), 0, st.s, drefs.p, npsf, md, dout.p);
+    SD_HIP(hipGetLastError());
+    SD_HIP(hipMemcpyAsync(avg, dout.p, md.n() * 4, hipMemcpyDeviceToHost, st.s));
+    SD_HIP(hipStreamSynchronize(st.s));
+}
+
+void max_projection(const float* img, const int64_t* dims, int min_dim, float* out, int64_t* out_dims, int* used_dim,
+                    int device) {
+    SD_CHECK(out_dims, SPIMDECON_ERR_ARG, "null argument");
+    const Dim3 s = dim3_of(dims, "image");
+    SD_CHECK(min_dim < 3, SPIMDECON_ERR_ARG, "min_dim must be < 3");
+    if (min_dim < 0) {  // the first smallest dimension (:116-128)
+        min_dim = 0;
+        for (int k = 0; k < 3; ++k)
+            if (dims[k] < dims[min_dim]) min_dim = k;
+    }
+    int j = 0;
+    for (int k = 0; k < 3; ++k)
+        if (k != min_dim) out_dims[j++] = dims[k];
+    if (used_dim) *used_dim = min_dim;
+    if (!out) return;
+    SD_CHECK(img, SPIMDECON_ERR_ARG, "null image");
+    check_device(device);
+    DeviceGuard guard(device);
+    Stream st;
+    DBuf<float> di(s.n());
+    SD_HIP(hipMemcpyAsync(di.p, img, s.n() * 4, hipMemcpyHostToDevice, st.s));
+    const int64_t no = out_dims[0] * out_dims[1];
+    DBuf<float> dout(no);
+    hipLaunchKernelGGL(k_max_projection, dim3(grid_for(no)), dim3(kPsfBlock), 0, st.s, di.p, s, min_dim, dout.p);
+    SD_HIP(hipGetLastError());
+    SD_HIP(hipMemcpyAsync(out, dout.p, no * 4, hipMemcpyDeviceToHost, st.s));
+    SD_HIP(hipStreamSynchronize(st.s));
+}
+
+}  // namespace spimdecon
+
+using namespace spimdecon;
+
+extern "C" int spim_psf_transformed_size(const int64_t psf_size[3], const double model[12], int64_t out_size[3],
+                                         double offset[3]) {
+    return guarded([&] { psf_transformed_size(psf_size, model, out_size, offset); });
+}
+
+extern "C" int spim_transform_psf(const float* psf, const int64_t psf_size[3], const double model[12], float* out,
+                                  int device) {
+    return guarded([&] { transform_psf(psf, psf_size, model, out, device); });
+}
+
+extern "C" int spim_extract_psf(const float* img, const int64_t dims[3], int img_on_device, const double* locations,
+                                int64_t nlocations, const int64_t psf_size[3], const double model[12],
+                                float* psf_original, float* psf_transformed, int device) {
+    return guarded([&] {
+        extract_psf(img, dims, img_on_device, locations, nlocations, psf_size, model, psf_original, psf_transformed,
+                    device);
+    });
+}
+
+extern "C" int spim_average_transformed_psf(int npsfs, const float* const* psfs, const int64_t* psf_dims,
+                                            float* avg, int64_t avg_dims[3], int device) {
+    return guarded([&] { average_transformed_psf(npsfs, psfs, psf_dims, avg, avg_dims, device); });
+}
+
+extern "C" int spim_max_projection(const float* img, const int64_t dims[3], int min_dim, float* out,
+                                   int64_t out_dims[2], int* used_dim, int device) {
+    return guarded([&] { max_projection(img, dims, min_dim, out, out_dims, used_dim, device); });
+}

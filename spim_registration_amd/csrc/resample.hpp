@@ -1,0 +1,100 @@
+// resample.hpp -- shared pieces of the affine resampling kernels (input_prep.hip,
+// psf.hip): the imglib2 AffineTransform3D inverse and NLinearInterpolator3D on
+// FloatType over the out-of-bounds strategies the reference uses
+// (extendMirrorSingle, extendPeriodic, extendZero), restated after
+// oracle/input_ref.py (parity unpinned: imglib2 is not in the reference tree).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace spimdecon {
+
+struct AffineInv {
+    double inv[9];   // inverse of the 3x3 part, row-major
+    double tr[3];    // translation of the model
+    double full[12]; // full inverse, row-major 3x4
+};
+
+enum Ext { kExtMirror = 0, kExtPeriodic = 1, kExtZero = 2 };
+
+__device__ __forceinline__ int mirror1(int i, int n) {
+    if (n == 1) return 0;
+    const int p = 2 * (n - 1);
+    int j = i % p;
+    if (j < 0) j += p;
+    return j >= n ? p - j : j;
+}
+
+template <int EXT>
+__device__ __forceinline__ float ext_at(const float* src, int sx, int sy, int sz, int x, int y, int z) {
+    if constexpr (EXT == kExtMirror) {
+        x = mirror1(x, sx);
+        y = mirror1(y, sy);
+        z = mirror1(z, sz);
+    } else if constexpr (EXT == kExtPeriodic) {
+        x %= sx;
+        y %= sy;
+        z %= sz;
+        x += x < 0 ? sx : 0;
+        y += y < 0 ? sy : 0;
+        z += z < 0 ? sz : 0;
+    } else {
+        if (x < 0 || y < 0 || z < 0 || x >= sx || y >= sy || z >= sz) return 0.0f;
+    }
+    return src[(int64_t(z) * sy + y) * sx + x];
+}
+
+// NLinearInterpolator3D: weights in double, FloatType.mul(double) / add per corner,
+// corner order 000, 100, 110, 010, 011, 111, 101, 001
+template <int EXT>
+__device__ float nlinear_at(const float* src, int sx, int sy, int sz, double p0, double p1, double p2) {
+    const double f0 = floor(p0), f1 = floor(p1), f2 = floor(p2);
+    const int xa = int(f0), ya = int(f1), za = int(f2);
+    const int xb = xa + 1, yb = ya + 1, zb = za + 1;
+    const double w0 = p0 - f0, w1 = p1 - f1, w2 = p2 - f2;
+    const double i0 = 1.0 - w0, i1 = 1.0 - w1, i2 = 1.0 - w2;
+    auto at = [&](int x, int y, int z) { return double(ext_at<EXT>(src, sx, sy, sz, x, y, z)); };
+    float acc = float(at(xa, ya, za) * (i0 * i1 * i2));
+    acc = acc + float(at(xb, ya, za) * (w0 * i1 * i2));
+    acc = acc + float(at(xb, yb, za) * (w0 * w1 * i2));
+    acc = acc + float(at(xa, yb, za) * (i0 * w1 * i2));
+    acc = acc + float(at(xa, yb, zb) * (i0 * w1 * w2));
+    acc = acc + float(at(xb, yb, zb) * (w0 * w1 * w2));
+    acc = acc + float(at(xb, ya, zb) * (w0 * i1 * w2));
+    acc = acc + float(at(xa, ya, zb) * (i0 * i1 * w2));
+    return acc;
+}
+
+inline AffineInv invert_model(const double* m) {
+    const double a00 = m[0], a01 = m[1], a02 = m[2], a10 = m[4], a11 = m[5], a12 = m[6];
+    const double a20 = m[8], a21 = m[9], a22 = m[10];
+    const double det = a00 * (a11 * a22 - a12 * a21) - a01 * (a10 * a22 - a12 * a20) +
+                       a02 * (a10 * a21 - a11 * a20);
+    SD_CHECK(det != 0.0 && std::isfinite(det), SPIMDECON_ERR_ARG, "affine model is not invertible");
+    AffineInv r{};
+    r.inv[0] = (a11 * a22 - a12 * a21) / det;
+    r.inv[1] = (a02 * a21 - a01 * a22) / det;
+    r.inv[2] = (a01 * a12 - a02 * a11) / det;
+    r.inv[3] = (a12 * a20 - a10 * a22) / det;
+    r.inv[4] = (a00 * a22 - a02 * a20) / det;
+    r.inv[5] = (a02 * a10 - a00 * a12) / det;
+    r.inv[6] = (a10 * a21 - a11 * a20) / det;
+    r.inv[7] = (a01 * a20 - a00 * a21) / det;
+    r.inv[8] = (a00 * a11 - a01 * a10) / det;
+    r.tr[0] = m[3];
+    r.tr[1] = m[7];
+    r.tr[2] = m[11];
+    for (int row = 0; row < 3; ++row) {
+        for (int c = 0; c < 3; ++c) r.full[4 * row + c] = r.inv[3 * row + c];
+        r.full[4 * row + 3] =
+            -(r.inv[3 * row] * r.tr[0] + r.inv[3 * row + 1] * r.tr[1] + r.inv[3 * row + 2] * r.tr[2]);
+    }
+    return r;
+}
+
+
+}  // namespace spimdecon

@@ -212,3 +212,24 @@ def test_input_prep_oracle_rules():
     imgs, ws, _ = ir.prepare_inputs([src, src], [ident, shifted], (0, 0, 0), (11, 7, 6), (0, 0, 0),
                                     (2, 2, 2), ir.VIRTUAL_WEIGHTS, osem_index=0, osem=3.0)
     assert max(float(w.max()) for w in ws) <= 1.0
+
+
+def test_psf_oracle_known_answers():
+    """ExtractPSF restatement: one bead at an integer location gives the
+    normalised crop; the identity model keeps the PSF; a pure z scaling keeps
+    the centre voxel and produces odd sizes (ExtractPSF.java:309-346)."""
+    from oracle import psf_ref as pr
+    rng = np.random.default_rng(3)
+    img = rng.random((12, 14, 16)).astype(np.float32)
+    p = pr.extract_psf_local(img, [(8.0, 7.0, 6.0)], (5, 5, 3))
+    np.testing.assert_array_equal(p, img[5:8, 5:10, 6:11])
+    q = pr.extract_psf_local(img, [(0.0, 0.0, 0.0)], (3, 3, 3))     # periodic wrap
+    assert q[0, 0, 0] == img[-1, -1, -1]
+    n = pr.normalize(p)
+    assert n.min() == 0 and n.max() == 1
+    np.testing.assert_array_equal(pr.transform_psf(n, np.eye(3, 4)), n)
+    size, off = pr.transformed_size((5, 5, 3), [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 2.0, 0])
+    assert size == [5, 5, 5] and off == [0.0, 0.0, 0.0]
+    t = pr.transform_psf(n, [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 2.0, 0])
+    np.testing.assert_array_equal(t[2], n[1])                        # centre plane kept
+    np.testing.assert_allclose(t[1], 0.5 * (n[0] + n[1]), rtol=1e-6)
