@@ -3,6 +3,7 @@
 # usage: tools/pmc_engine.sh OUTDIR [extra bench args]
 set -o pipefail
 OUT=$1; shift
+mkdir -p $OUT
 export TMPDIR=/tmp
 B="python3 bench.py --steps 1 --warmup 0 --no-timing --no-cpu-baseline $*"
 R="--kernel-include-regex k_xpass|k_xrows|k_xtile|k_colpass|k_col2f"
