@@ -178,7 +178,7 @@ def main():
             # algorithmic HBM bytes per launch of each fused pass (DESIGN.md "kernels")
             classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, 16),
                        ("z_convolve", 0, 0, 24), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
-                       ("stats_reduce", 0, 0, 0)]
+                       ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 24)]
             b_iter = V * ((12 + 2 * wb) * N + 144.0 * S)
             model = "V*((12+2w)N + 144S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes"
         else:

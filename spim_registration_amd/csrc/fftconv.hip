@@ -640,15 +640,23 @@ static int col_grid_rounds() {
 }
 #define kColGridRounds col_grid_rounds()
 
-// two-factor column pass; false when the buffer-offset path does not apply
+// two-factor column pass; false when the buffer-offset path does not apply.
+// MODE 5: K is the compact kernel (2*kc+1 z-planes, engine_kernel_compact).
 template <int AXIS, int MODE>
-bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s,
+                  int tx0 = 0, int ntxb = -1, int kc = 0) {
     const int TX = k2fTX;  // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
     const int L = f.L;
-    const size_t lds = size_t(L * TX + L) * sizeof(float2);
+    const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
+    const size_t lds = size_t(L * TX + L + (MODE == 5 ? f.n2 * TX : 0)) * sizeof(float2);
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
+    const uint64_t kbytes = MODE == 5 ? uint64_t(kplanes) * p.Hp * p.g.My * sizeof(float2)
+                                      : (MODE >= 2 ? bytes : 0);
     if (lds > 80 * 1024 || bytes >= (uint64_t(1) << 31)) return false;
-    const int64_t ntiles = (p.Hp / TX) * (AXIS == 1 ? p.g.Mz : p.g.My);
+    if (MODE == 5 && (AXIS != 2 || kplanes > f.n2)) return false;
+    if (ntxb < 0) ntxb = int(p.Hp / TX);
+    SD_CHECK(tx0 >= 0 && ntxb > 0 && tx0 + ntxb <= p.Hp / TX, SPIMDECON_ERR_ARG, "bad column band");
+    const int64_t ntiles = int64_t(ntxb) * (AXIS == 1 ? p.g.Mz : p.g.My);
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
     const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
     const int n1 = f.n1, n2 = f.n2;
@@ -658,7 +666,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
         SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T>),         \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
         hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T>), dim3(grid), dim3(T * 32), lds, s, p.g, p.Hp,   \
-                           f.tw, C, K, uint32_t(bytes));                                                   \
+                           f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes));                 \
         done = true;                                                                                       \
     }
 #define SD_2F_C(A, B) \
@@ -801,6 +809,50 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
     SD_HIP(hipStreamSynchronize(s));
 }
 
+bool engine_kernel_compact_ok(const SpectralPlan& p) {
+    const int kc = p.g.cz;
+    return p.fz.n1 && 2 * kc + 1 <= p.fz.n2 &&
+           size_t(p.fz.L * k2fTX + p.fz.L + p.fz.n2 * k2fTX) * sizeof(float2) <= 80 * 1024 &&
+           uint64_t(p.spectrum_elems()) * sizeof(float2) < (uint64_t(1) << 31);
+}
+
+int64_t engine_kernel_compact_elems(const SpectralPlan& p) { return int64_t(2 * p.g.cz + 1) * p.g.My * p.Hp; }
+
+void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz, float scale,
+                           float2* work, float2* Kc, hipStream_t s) {
+    // x and y transforms of the placed kernel (work = full spectrum buffer), then the
+    // z-planes qz in [-kc, kc] (wrapped) -> Kc[qz + kc]: all the z pass needs, since
+    // the placed kernel is zero outside them (|qz| <= kz/2 <= cz)
+    SD_CHECK(engine_kernel_compact_ok(p), SPIMDECON_ERR_ARG, "compact kernel path not available");
+    SD_CHECK(kz / 2 <= p.g.cz, SPIMDECON_ERR_ARG, "kernel z half size exceeds the halo");
+    XArgs a = base_args(p);
+    a.Cout = work;
+    a.kern = d_kernel;
+    a.kx = kx;
+    a.ky = ky;
+    a.kz = kz;
+    a.kscale = scale;
+    DBuf<int> all(size_t(p.g.My * p.g.Mz));
+    SD_HIP(hipMemsetAsync(all.p, 0, all.bytes(), s));
+    a.row_mirror = all.p;
+    a.row_one = all.p;
+    launch_x<XM_KERNEL>(a, Store::F32, p, s);
+    launch_col<1, false, 0>(p, p.fy, work, nullptr, s);
+    const int kc = p.g.cz;
+    const size_t plane = size_t(p.g.My * p.Hp) * sizeof(float2);
+    SD_HIP(hipMemcpyAsync(Kc + size_t(kc) * p.g.My * p.Hp, work, size_t(kc + 1) * plane,
+                          hipMemcpyDeviceToDevice, s));
+    if (kc > 0)
+        SD_HIP(hipMemcpyAsync(Kc, work + size_t(p.g.Mz - kc) * p.g.My * p.Hp, size_t(kc) * plane,
+                              hipMemcpyDeviceToDevice, s));
+    SD_HIP(hipStreamSynchronize(s));
+}
+
+void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
+    const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz);
+    SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
+}
+
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
     if (inv) launch_col<1, true, 0>(p, p.fy, C, nullptr, s);
     else launch_col<1, false, 0>(p, p.fy, C, nullptr, s);
@@ -811,6 +863,32 @@ void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t
     // as two launches (0.61 ms)
     if (K) launch_col<2, false, 1>(p, p.fz, C, K, s);
     else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
+}
+
+int engine_band_tiles() {
+    static const int b = [] {
+        const char* e = std::getenv("SPIMDECON_BAND");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return b;
+}
+
+bool engine_convolve_banded(const SpectralPlan& p, float2* C, const float2* K, bool compact, int band,
+                            hipStream_t s) {
+    // y forward, z (forward * K * inverse) and y inverse over bands of `band` 16-bin tile
+    // columns: a band's spectrum (band * 16 * My * Mz * 8 B) stays in the Infinity Cache
+    // between the three passes, so only the first read and the last write reach HBM
+    if (band <= 0 || !p.fy.n1 || !p.fz.n1 || !K) return false;
+    const int nt = int(p.Hp / k2fTX);
+    for (int t0 = 0; t0 < nt; t0 += band) {
+        const int nb = std::min(band, nt - t0);
+        if (!launch_col2f<1, 0>(p, p.fy, C, nullptr, s, t0, nb)) return false;
+        if (!(compact ? launch_col2f<2, 5>(p, p.fz, C, K, s, t0, nb, p.g.cz)
+                      : launch_col2f<2, 4>(p, p.fz, C, K, s, t0, nb)))
+            return false;
+        if (!launch_col2f<1, 1>(p, p.fy, C, nullptr, s, t0, nb)) return false;
+    }
+    return true;
 }
 
 PairRanges all_pairs(const SpectralPlan& p) {

@@ -64,10 +64,25 @@ void engine_forward_psi(const SpectralPlan& p, const float* psi, float2* C, hipS
 // small kernel (kx,ky,kz) -> full 3D spectrum in Kspec (scaled), uses `work` as scratch-free in place
 void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz,
                             float scale, float2* Kspec, hipStream_t s);
+// compact kernel spectra (two-factor z length only): the x and y transforms of the
+// placed kernel on its 2*cz+1 non-zero z-planes, [2cz+1][My][Hp]; the z pass
+// (engine_zpass_compact) computes the z transform in its tiles.  `work` is a
+// full spectrum_elems() scratch buffer.
+bool engine_kernel_compact_ok(const SpectralPlan& p);
+int64_t engine_kernel_compact_elems(const SpectralPlan& p);
+void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz, float scale,
+                           float2* work, float2* Kc, hipStream_t s);
+void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s);
 // Y pass: in-place complex FFT along y (inverse when inv)
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 // Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
+// y forward + z convolve + y inverse over bands of `band` tile columns (Infinity-Cache
+// resident); false (nothing launched) when the two-factor path does not apply.
+// engine_band_tiles(): the band width from env SPIMDECON_BAND (0 = unbanded)
+bool engine_convolve_banded(const SpectralPlan& p, float2* C, const float2* K, bool compact, int band,
+                            hipStream_t s);
+int engine_band_tiles();
 // packed row pairs (rows 2i, 2i+1 of the My*Mz padded rows) an x pass covers:
 // [b0, b0 + n0) then [b1, b1 + n1)
 struct PairRanges {

@@ -209,14 +209,28 @@ void Session::build_spectra() {
             SD_HIP(hipMemsetAsync(sl.C2.p, 0, sl.C2.bytes(), stream_));
             sl.e1spec.clear();
             sl.e2spec.clear();
+            // compact kernels (2cz+1 z-planes, z transform in the z pass) unless
+            // SPIMDECON_ZK=full / =reg asks for the full spectra (A/B runs)
+            const char* zk = std::getenv("SPIMDECON_ZK");  // read per session (tests toggle it)
+            const bool full_k = zk && (zk[0] == 'f' || zk[0] == 'r');
+            sl.kcompact = !full_k && engine_kernel_compact_ok(sl.sp);
+            DBuf<float2> work;
+            if (sl.kcompact) work.alloc(ne);
             for (int v = 0; v < nviews_; ++v) {
                 for (int which = 0; which < 2; ++which) {
                     const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
                     kd.alloc(hk.data.size());
                     SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
-                    DBuf<float2> spec(ne);
-                    engine_kernel_spectrum(sl.sp, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p,
-                                           stream_);
+                    DBuf<float2> spec;
+                    if (sl.kcompact) {
+                        spec.alloc(size_t(engine_kernel_compact_elems(sl.sp)));
+                        engine_kernel_compact(sl.sp, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, work.p,
+                                              spec.p, stream_);
+                    } else {
+                        spec.alloc(ne);
+                        engine_kernel_spectrum(sl.sp, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p,
+                                               stream_);
+                    }
                     (which == 0 ? sl.e1spec : sl.e2spec).push_back(std::move(spec));
                 }
             }
@@ -473,9 +487,10 @@ void Session::run_rocfft(int iters, double lambda) {
 }
 
 // timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 fused z pass,
-// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce
+// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce, 7 banded y-z-y convolve
 void Session::run_engine(int iters, double lambda) {
     const int V = nviews_;
+    const int band = engine_band_tiles();
     const bool halo = slabs_.size() > 1 || p_.nranks > 1;
     // overlap: the x pass writes the planes the neighbours need first; their exchange
     // (xstream_) runs while the x pass covers the rest of the slab
@@ -501,8 +516,17 @@ void Session::run_engine(int iters, double lambda) {
         for (int v = 0; v < V; ++v) {
             const bool last = (it == iters - 1) && (v == V - 1);
             for (auto& sl : slabs_) {  // convolve1
+                if (band > 0) {
+                    tstart(7);
+                    const bool banded = engine_convolve_banded(sl.sp, sl.C1.p, sl.e1spec[v].p, sl.kcompact, band, stream_);
+                    tstop();
+                    if (banded) continue;
+                }
                 tstart(2); engine_ypass(sl.sp, sl.C1.p, false, stream_); tstop();
-                tstart(3); engine_zpass(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_); tstop();
+                tstart(3);
+                if (sl.kcompact) engine_zpass_compact(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_);
+                else engine_zpass(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_);
+                tstop();
                 tstart(2); engine_ypass(sl.sp, sl.C1.p, true, stream_); tstop();
             }
             // quotient (+ forward x of the quotient) and its halo exchange
@@ -526,8 +550,17 @@ void Session::run_engine(int iters, double lambda) {
                 exchange(false, stream_);
             }
             for (auto& sl : slabs_) {  // convolve2
+                if (band > 0) {
+                    tstart(7);
+                    const bool banded = engine_convolve_banded(sl.sp, sl.C2.p, sl.e2spec[v].p, sl.kcompact, band, stream_);
+                    tstop();
+                    if (banded) continue;
+                }
                 tstart(2); engine_ypass(sl.sp, sl.C2.p, false, stream_); tstop();
-                tstart(3); engine_zpass(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_); tstop();
+                tstart(3);
+                if (sl.kcompact) engine_zpass_compact(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_);
+                else engine_zpass(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_);
+                tstop();
                 tstart(2); engine_ypass(sl.sp, sl.C2.p, true, stream_); tstop();
             }
             // update (+ forward x of the next psi) and its halo exchange

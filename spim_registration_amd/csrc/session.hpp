@@ -39,7 +39,8 @@ struct SlabState {
     DBuf<float> Ra, Rb;                       // rocFFT backend work volumes
     SpectralPlan sp;                           // engine backend
     DBuf<float2> C1, C2;
-    std::vector<DBuf<float2>> e1spec, e2spec;
+    std::vector<DBuf<float2>> e1spec, e2spec;  // full kernel spectra, or compact ones (kcompact)
+    bool kcompact = false;
     DBuf<double> partials;
     DBuf<const void*> img_ptrs;
     std::unique_ptr<FftPlan3D> fft;
