@@ -74,8 +74,9 @@ def pmc_traffic(cls, M, args):
         return None, None
     for name, ent in d["kernels"].items():
         if name.startswith(PMC_KERNELS.get(cls, ())):
-            if cls == "z_convolve" and not name.rstrip(">").endswith("2"):
-                continue   # the fused z pass is MODE 2
+            targs = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
+            if cls == "z_convolve" and name.startswith("k_col2f") and targs[3] not in ("2", "4", "5"):
+                continue   # the fused z pass: k_col2f MODE 2/4/5 (5 = compact kernels)
             return int(ent["hbm_bytes_per_launch"]), f"{d['file']}: {name}"
     return None, None
 
@@ -175,12 +176,15 @@ def main():
         S = (M[0] // 2 + 1) * M[1] * M[2]   # half-spectrum elements (algorithmic, unpadded)
         wb = 2 if args.fp16 else 4          # bytes per img / weight voxel
         if args.backend == "engine":
-            # algorithmic HBM bytes per launch of each fused pass (DESIGN.md "kernels")
+            # algorithmic HBM bytes per launch of each fused pass (DESIGN.md "kernels"); the
+            # z pass reads its kernel's stored z-planes: 2cz+1 of Mz when compact
+            kz = 8.0 * sess.kernel_planes(0) / M[2]
             classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, 16),
-                       ("z_convolve", 0, 0, 24), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
-                       ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 24)]
-            b_iter = V * ((12 + 2 * wb) * N + 144.0 * S)
-            model = "V*((12+2w)N + 144S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes"
+                       ("z_convolve", 0, 0, 16 + kz), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
+                       ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 16 + kz)]
+            b_iter = V * ((12 + 2 * wb) * N + (128.0 + 2 * kz) * S)
+            model = (f"V*((12+2w)N + (128+2k)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
+                     f"k = 8*kernel z-planes/Mz = {kz:.3f}")
         else:
             classes = [("update_pad", 8 + wb, N, 0), ("quotient_pad", wb, N, 0), ("r2c", 0, 0, 0),
                        ("spec_mul", 0, 0, 0), ("c2r", 0, 0, 0), ("halo_exchange", 0, 0, 0),

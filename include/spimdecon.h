@@ -198,6 +198,9 @@ float* mvd_psi_device(mvd_session* h, int slab);
 
 /* padded FFT dims {Mx, My, Mz} of local slab s (info/bench) */
 int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3);
+/* z-planes of each stored kernel spectrum (info/bench): 2*cz+1 when the engine
+ * keeps compact kernels (the z pass builds their z transform), else Mz */
+int mvd_kernel_planes(mvd_session* h, int slab, int* planes);
 /* HIP stream the session launches on (hipStream_t as void*) */
 void* mvd_stream(mvd_session* h);
 /* per-kernel timing: when enabled, mvd_run records HIP events around every

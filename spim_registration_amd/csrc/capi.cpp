@@ -259,6 +259,10 @@ int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3) {
     return guarded([&] { SESSION(h); SD_CHECK(out3, SPIMDECON_ERR_ARG, "null"); S.fft_dims(slab, out3); });
 }
 
+int mvd_kernel_planes(mvd_session* h, int slab, int* planes) {
+    return guarded([&] { SESSION(h); SD_CHECK(planes, SPIMDECON_ERR_ARG, "null"); *planes = S.kernel_planes(slab); });
+}
+
 void* mvd_stream(mvd_session* h) {
     void* r = nullptr;
     guarded([&] { SESSION(h); r = S.stream(); });

@@ -539,28 +539,36 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
         const char* e = std::getenv("SPIMDECON_X2F");
         return !(e && e[0] == '0');
     }();
+    static const int np_env = [] {  // row pairs per tile, SPIMDECON_XTP=8|16 for A/B runs
+        const char* e = std::getenv("SPIMDECON_XTP");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 8 || v == 16 ? v : 0;
+    }();
+    const int np = np_env ? np_env : (MODE == XM_UPDATE ? 8 : 16);
     XArgs b;
     if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
-    const size_t lds = size_t(L + 1 + kXtPairs * (L + 1)) * sizeof(float2);
+    const size_t lds = size_t(L + 1 + np * (L + 1)) * sizeof(float2);
     if (lds > 160 * 1024) return 0;
-    const int64_t ntiles = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, kXtPairs));
+    const int64_t ntiles = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, np));
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-    const unsigned grid = unsigned(std::min<int64_t>({ntiles, 256 * per_cu, 4096}));
+    const unsigned grid = unsigned(std::min<int64_t>({ntiles, 256 * per_cu, 2048}));
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
-#define SD_XT(SV, A, B, TK)                                                                             \
-    if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                            \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK>),       \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
-        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK>), dim3(grid), dim3(kXtThreads), lds, s, b);   \
-        done = true;                                                                                   \
+#define SD_XT(SV, A, B, TK, NP)                                                                          \
+    if (!done && np == NP && sv == SV && L == (A) * (B) && tik == TK) {                                 \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, NP>),    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));              \
+        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, NP>), dim3(grid), dim3(NP * 32), lds, s, b);   \
+        done = true;                                                                                    \
     }
-#define SD_XT_S(A, B) \
-    SD_XT(0, A, B, false) SD_XT(1, A, B, false) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true) SD_XT(1, A, B, true) }
+#define SD_XT_N(A, B, NP) \
+    SD_XT(0, A, B, false, NP) SD_XT(1, A, B, false, NP) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true, NP) SD_XT(1, A, B, true, NP) }
+#define SD_XT_S(A, B) SD_XT_N(A, B, 16) SD_XT_N(A, B, 8)
     SD_X2F_SIZES(SD_XT_S)
 #undef SD_XT_S
+#undef SD_XT_N
 #undef SD_XT
     if (!done) return 0;
     SD_HIP(hipGetLastError());

@@ -627,4 +627,12 @@ void Session::fft_dims(int slab, int64_t* out3) const {
     for (int d = 0; d < 3; ++d) out3[d] = slabs_[slab].pd.M[d];
 }
 
+int Session::kernel_planes(int slab) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
+    const SlabState& sl = slabs_[slab];
+    if (backend_ != 0) return int(sl.pd.M[2]);
+    return sl.kcompact ? int(2 * sl.sp.g.cz + 1) : int(sl.sp.g.Mz);
+}
+
 }  // namespace spimdecon

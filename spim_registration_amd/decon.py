@@ -239,6 +239,12 @@ class Session:
         check(self.lib.mvd_fft_dims(self.h, int(slab), out))
         return tuple(out)
 
+    def kernel_planes(self, slab=0):
+        """z-planes per stored kernel spectrum (2*cz+1 compact, else Mz)."""
+        out = C.c_int()
+        check(self.lib.mvd_kernel_planes(self.h, int(slab), C.byref(out)))
+        return out.value
+
     def enable_timing(self, on=True):
         check(self.lib.mvd_enable_timing(self.h, int(on)))
 
