@@ -21,22 +21,20 @@ namespace {
 // so that the RL pointwise steps keep the reference's float op order; those use
 // explicit __f*_rn intrinsics).  The spectra are not bit-matched to any
 // reference anyway, and FMA is the more accurate of the two.
+// Written on 2-wide float vectors so that every complex op is one packed VALU op
+// (v_pk_mul/add/fma_f32 with operand swizzles and negations folded in): a complex
+// multiply is a v_pk_mul + a v_pk_fma instead of scalar ops and register moves.
+typedef float sd_v2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sd_v2 v2_(float2 a) { return sd_v2{a.x, a.y}; }
+__device__ __forceinline__ float2 f2_(sd_v2 a) { return make_float2(a.x, a.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-#pragma clang fp contract(fast)
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    const sd_v2 A = v2_(a), B = v2_(b);
+    const sd_v2 t = A.xx * B;                                              // (ax bx, ax by)
+    return f2_(__builtin_elementwise_fma(A.yy, sd_v2{-B.y, B.x}, t));      // (- ay by, + ay bx)
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
-#pragma clang fp contract(fast)
-    return make_float2(a.x + b.x, a.y + b.y);
-}
-__device__ __forceinline__ float2 csub(float2 a, float2 b) {
-#pragma clang fp contract(fast)
-    return make_float2(a.x - b.x, a.y - b.y);
-}
-__device__ __forceinline__ float2 cscale(float2 a, float s) {
-#pragma clang fp contract(fast)
-    return make_float2(a.x * s, a.y * s);
-}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return f2_(v2_(a) + v2_(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return f2_(v2_(a) - v2_(b)); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return f2_(v2_(a) * sd_v2{s, s}); }
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
