@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--views", type=int, default=6)
     ap.add_argument("--size", type=int, default=512, help="per-GPU cube edge")
+    ap.add_argument("--shape", type=int, nargs=3, metavar=("X", "Y", "Z"),
+                    help="per-GPU slab x y z (overrides --size; z-slabs stack over ranks)")
     ap.add_argument("--ksize", type=int, default=25)
     ap.add_argument("--psftype", default="INDEPENDENT")
     ap.add_argument("--lam", type=float, default=0.0)
@@ -123,14 +125,14 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
     comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
 
-    n = args.size
+    nx, ny, nz = args.shape if args.shape else (args.size,) * 3
     V = args.views
-    nz_g = n * world
-    imgs, ws, psfs = synthetic.make_views_torch((n, n, n), V, config_id=1 + rank,
+    nz_g = nz * world
+    imgs, ws, psfs = synthetic.make_views_torch((nz, ny, nx), V, config_id=1 + rank,
                                                 ksize=(args.ksize,) * 3, device=f"cuda:{local}")
     torch.cuda.synchronize()
-    sess = Session((n, n, n), device=local, nranks=world, rank=rank, comm_id=comm_id,
-                   nz_global=nz_g, z_offset=rank * n, storage_fp16=args.fp16,
+    sess = Session((nx, ny, nz), device=local, nranks=world, rank=rank, comm_id=comm_id,
+                   nz_global=nz_g, z_offset=rank * nz, storage_fp16=args.fp16,
                    fft_backend=args.backend, fft_pad_policy=args.pad_policy)
     for i, w, k in zip(imgs, ws, psfs):
         sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
@@ -159,7 +161,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     ms_per_step = dt / max(args.steps, 1) * 1e3
-    n_vox_total = n * n * nz_g
+    n_vox_total = nx * ny * nz_g
     value = n_vox_total * args.steps / dt / 1e6
 
     # roofline pass: HIP events on the session stream around every kernel class
@@ -171,7 +173,7 @@ def main():
         sess.run(2, args.lam)
         tm = sess.timing()
         sess.enable_timing(False)
-        N = n ** 3
+        N = nx * ny * nz
         Mlog = M[0] * M[1] * M[2]
         S = (M[0] // 2 + 1) * M[1] * M[2]   # half-spectrum elements (algorithmic, unpadded)
         wb = 2 if args.fp16 else 4          # bytes per img / weight voxel
@@ -239,9 +241,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" + ("(fp16 img/w storage)" if args.fp16 else ""),
             "data": "synthetic (seeded bead stacks generated on the GPU, SURVEY 8d)",
-            "config": {"workload": f"{V}-view {n}^3 per GPU (global {n}x{n}x{nz_g}), "
+            "config": {"workload": (f"{V}-view {nx}^3" if nx == ny == nz else f"{V}-view {nx}x{ny}x{nz}")
+                                   + f" per GPU (global {nx}x{ny}x{nz_g}), "
                                    f"{args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}",
-                       "views": V, "volume_xyz": [n, n, nz_g], "psf": [args.ksize] * 3,
+                       "views": V, "volume_xyz": [nx, ny, nz_g], "psf": [args.ksize] * 3,
                        "fft_dims_xyz": list(M), "parallelism": f"z-slab x{world} (RCCL halo)"},
             "roofline": roofline,
             "roofline_iteration": it_roof,

@@ -512,7 +512,7 @@ XArgs base_args(const SpectralPlan& p) {
 }
 
 // two-factor x tiles: lengths >= 256 of the fast-path table
-#define SD_X2F_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24) M(20, 32) M(25, 32)
+#define SD_X2F_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24) M(20, 32) M(25, 32) M(30, 35)
 
 bool aligned_to(const void* q, size_t n) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % n == 0; }
 
@@ -554,12 +554,13 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
-#define SD_XT(SV, A, B, TK, NP)                                                                          \
-    if (!done && np == NP && sv == SV && L == (A) * (B) && tik == TK) {                                 \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, NP>),    \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));              \
-        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, NP>), dim3(grid), dim3(NP * 32), lds, s, b);   \
-        done = true;                                                                                    \
+#define SD_XT(SV, A, B, TK, NP)                                                                            \
+    if (!done && np == NP && sv == SV && L == (A) * (B) && tik == TK) {                                   \
+        constexpr int TRv = SD_2F_TR(A, B);                                                               \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, NP, TRv>), \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                \
+        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, NP, TRv>), dim3(grid), dim3(NP * TRv), lds, s, b); \
+        done = true;                                                                                      \
     }
 #define SD_XT_N(A, B, NP) \
     SD_XT(0, A, B, false, NP) SD_XT(1, A, B, false, NP) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true, NP) SD_XT(1, A, B, true, NP) }
@@ -658,7 +659,11 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
     const uint64_t kbytes = MODE == 5 ? uint64_t(kplanes) * p.Hp * p.g.My * sizeof(float2)
                                       : (MODE >= 2 ? bytes : 0);
-    if (lds > 80 * 1024 || bytes >= (uint64_t(1) << 31)) return false;
+    const int tr = (f.n1 > 32 || f.n2 > 32) ? 64 : 32;  // SD_2F_TR
+    // the fused z modes hold two length-N2 vectors per thread: TR = 64 (N2 > 32) would
+    // spill, so long lengths run them on the Stockham column pass
+    if (MODE >= 2 && tr == 64) return false;
+    if (lds > (tr == 64 ? 160 : 80) * 1024 || bytes >= (uint64_t(1) << 31)) return false;
     if (MODE == 5 && (AXIS != 2 || kplanes > f.n2)) return false;
     if (ntxb < 0) ntxb = int(p.Hp / TX);
     SD_CHECK(tx0 >= 0 && ntxb > 0 && tx0 + ntxb <= p.Hp / TX, SPIMDECON_ERR_ARG, "bad column band");
@@ -668,12 +673,15 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     const int n1 = f.n1, n2 = f.n2;
     bool done = false;
 #define SD_2F_C1(A, B, T)                                                                                  \
-    if (!done && n1 == (A) && n2 == (B) && TX == (T)) {                                                    \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T>),         \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
-        hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T>), dim3(grid), dim3(T * 32), lds, s, p.g, p.Hp,   \
-                           f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes));                 \
-        done = true;                                                                                       \
+    if constexpr (MODE < 2 || SD_2F_TR(A, B) == 32) {                                                      \
+        if (!done && n1 == (A) && n2 == (B) && TX == (T)) {                                                \
+            constexpr int TRv = SD_2F_TR(A, B);                                                            \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv>), \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
+            hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv>), dim3(grid), dim3(T * TRv), lds, s,     \
+                               p.g, p.Hp, f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes));  \
+            done = true;                                                                                   \
+        }                                                                                                  \
     }
 #define SD_2F_C(A, B) \
     SD_2F_C1(A, B, 16)
@@ -817,7 +825,7 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
 
 bool engine_kernel_compact_ok(const SpectralPlan& p) {
     const int kc = p.g.cz;
-    return p.fz.n1 && 2 * kc + 1 <= p.fz.n2 &&
+    return p.fz.n1 && p.fz.n1 <= 32 && p.fz.n2 <= 32 && 2 * kc + 1 <= p.fz.n2 &&  // MODE 5 is TR = 32 only
            size_t(p.fz.L * k2fTX + p.fz.L + p.fz.n2 * k2fTX) * sizeof(float2) <= 80 * 1024 &&
            uint64_t(p.spectrum_elems()) * sizeof(float2) < (uint64_t(1) << 31);
 }

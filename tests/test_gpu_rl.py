@@ -141,7 +141,11 @@ def test_engine_matches_rocfft_backend(gpu, shape, ksize):
 @pytest.mark.parametrize("policy", ["fast", "smooth"])
 @pytest.mark.parametrize("shape,ksize", [((20, 24, 28), (7, 9, 11)), ((33, 17, 46), (5, 7, 3)),
                                          ((30, 61, 40), (9, 5, 7)), ((12, 14, 500), (3, 3, 25)),
-                                         ((10, 500, 12), (3, 25, 3)), ((500, 10, 12), (25, 3, 3))])
+                                         ((10, 500, 12), (3, 25, 3)), ((500, 10, 12), (25, 3, 3)),
+                                         # M = 1050 = 30*35: the TR = 64 two-factor passes (x tile,
+                                         # y column pass; the z pass falls back to Stockham)
+                                         ((12, 14, 1024), (3, 3, 27)), ((10, 1024, 12), (3, 27, 3)),
+                                         ((1024, 10, 12), (27, 3, 3))])
 def test_engine_pad_policies(gpu, shape, ksize, policy):
     """Two-factor register passes ("fast") and Stockham passes ("smooth") agree
     with the rocFFT backend and the oracle."""
