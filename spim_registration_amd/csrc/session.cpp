@@ -172,7 +172,9 @@ void Session::build_spectra() {
         g.My = sl.pd.M[1];
         g.Mz = sl.pd.M[2];
         g.Sx = sl.pd.Sx();
-        sl.partials.alloc(2 * 256 * 16);
+        // stats partials: one {sum, max} per x-pass block; the x tiles may run one
+        // tile (>= 1 row pair) per block, split over two launches (boundary + rest)
+        sl.partials.alloc(size_t(2) * std::max<int64_t>(256 * 16, (g.My * g.Mz + 1) / 2 + 64));
         std::vector<const void*> ptrs(nviews_);
         for (int v = 0; v < nviews_; ++v) ptrs[v] = sl.img[v].p;
         sl.img_ptrs.alloc(nviews_);
