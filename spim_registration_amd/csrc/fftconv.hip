@@ -542,10 +542,9 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
         const int v = e ? std::atoi(e) : 0;
         return v == 8 || v == 16 ? v : 0;
     }();
-    // 8 pairs for the update tiles and for 64-thread pairs (2 blocks per CU: 0.90 vs
-    // 1.05 ms quotient at L = 1050), 16 for the 32-thread quotient tiles
-    const bool tr64 = p.fx.n1 > 32 || p.fx.n2 > 32;
-    const int np = np_env ? np_env : (MODE == XM_UPDATE || tr64 ? 8 : 16);
+    // 8 pairs per tile (one tile per block): quotient 0.40 vs 0.43 ms with 16 pairs
+    // and 0.45 with 4, update 0.52 vs 0.58 / 0.54 ms; at L = 1050 quotient 0.90 vs 1.05 ms
+    const int np = np_env ? np_env : 8;
     XArgs b;
     if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
