@@ -40,8 +40,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--views", type=int, default=6)
     ap.add_argument("--size", type=int, default=512, help="per-GPU cube edge")
     ap.add_argument("--shape", type=int, nargs=3, metavar=("X", "Y", "Z"),
