@@ -40,6 +40,19 @@ template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
     return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
+// a + mul_mi<INV>(d) and a - mul_mi<INV>(d) as ONE v_pk_fma (d swizzled, times
+// (+-1, -+1), plus a): exact like the add, but without the xor + mov the separate
+// swap-and-negate cost
+template <bool INV>
+__device__ __forceinline__ float2 cadd_mi(float2 a, float2 d) {
+    const sd_v2 D = v2_(d);
+    return f2_(__builtin_elementwise_fma(D.yx, INV ? sd_v2{-1.0f, 1.0f} : sd_v2{1.0f, -1.0f}, v2_(a)));
+}
+template <bool INV>
+__device__ __forceinline__ float2 csub_mi(float2 a, float2 d) {
+    const sd_v2 D = v2_(d);
+    return f2_(__builtin_elementwise_fma(D.yx, INV ? sd_v2{1.0f, -1.0f} : sd_v2{-1.0f, 1.0f}, v2_(a)));
+}
 
 __device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
     if (n == 1) return 0;
@@ -100,16 +113,15 @@ __device__ __forceinline__ void dft(float2* a) {
         const float2 m = csub(a[0], cscale(s, 0.5f));
         const float2 d = cscale(csub(a[1], a[2]), 0.86602540378443864676f);
         a[0] = cadd(a[0], s);
-        const float2 id = mul_mi<INV>(d);  // -i*d forward
-        a[1] = cadd(m, id);
-        a[2] = csub(m, id);
+        a[1] = cadd_mi<INV>(m, d);  // m - i*d forward
+        a[2] = csub_mi<INV>(m, d);
     } else if constexpr (R == 4) {
         const float2 s0 = cadd(a[0], a[2]), d0 = csub(a[0], a[2]);
-        const float2 s1 = cadd(a[1], a[3]), d1 = mul_mi<INV>(csub(a[1], a[3]));
+        const float2 s1 = cadd(a[1], a[3]), d1 = csub(a[1], a[3]);
         a[0] = cadd(s0, s1);
         a[2] = csub(s0, s1);
-        a[1] = cadd(d0, d1);
-        a[3] = csub(d0, d1);
+        a[1] = cadd_mi<INV>(d0, d1);
+        a[3] = csub_mi<INV>(d0, d1);
     } else if constexpr (R == 5) {
         constexpr float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
         constexpr float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
@@ -117,13 +129,13 @@ __device__ __forceinline__ void dft(float2* a) {
         const float2 d1 = csub(a[1], a[4]), d2 = csub(a[2], a[3]);
         const float2 m1 = cadd(a[0], cadd(cscale(b1, c1), cscale(b2, c2)));
         const float2 m2 = cadd(a[0], cadd(cscale(b1, c2), cscale(b2, c1)));
-        const float2 n1 = mul_mi<INV>(cadd(cscale(d1, s1), cscale(d2, s2)));
-        const float2 n2 = mul_mi<INV>(csub(cscale(d1, s2), cscale(d2, s1)));
+        const float2 n1 = cadd(cscale(d1, s1), cscale(d2, s2));
+        const float2 n2 = csub(cscale(d1, s2), cscale(d2, s1));
         a[0] = cadd(a[0], cadd(b1, b2));
-        a[1] = cadd(m1, n1);
-        a[4] = csub(m1, n1);
-        a[2] = cadd(m2, n2);
-        a[3] = csub(m2, n2);
+        a[1] = cadd_mi<INV>(m1, n1);
+        a[4] = csub_mi<INV>(m1, n1);
+        a[2] = cadd_mi<INV>(m2, n2);
+        a[3] = csub_mi<INV>(m2, n2);
     } else {
         static_assert(R == 7, "radix 2, 3, 4, 5, 7 only");
         constexpr float c1 = 0.62348980185873353053f, c2 = -0.22252093395631440429f,
@@ -135,16 +147,16 @@ __device__ __forceinline__ void dft(float2* a) {
         const float2 r1 = cadd(a[0], cadd(cscale(b1, c1), cadd(cscale(b2, c2), cscale(b3, c3))));
         const float2 r2 = cadd(a[0], cadd(cscale(b1, c2), cadd(cscale(b2, c3), cscale(b3, c1))));
         const float2 r3 = cadd(a[0], cadd(cscale(b1, c3), cadd(cscale(b2, c1), cscale(b3, c2))));
-        const float2 i1 = mul_mi<INV>(cadd(cscale(d1, s1), cadd(cscale(d2, s2), cscale(d3, s3))));
-        const float2 i2 = mul_mi<INV>(csub(cscale(d1, s2), cadd(cscale(d2, s3), cscale(d3, s1))));
-        const float2 i3 = mul_mi<INV>(cadd(csub(cscale(d1, s3), cscale(d2, s1)), cscale(d3, s2)));
+        const float2 i1 = cadd(cscale(d1, s1), cadd(cscale(d2, s2), cscale(d3, s3)));
+        const float2 i2 = csub(cscale(d1, s2), cadd(cscale(d2, s3), cscale(d3, s1)));
+        const float2 i3 = cadd(csub(cscale(d1, s3), cscale(d2, s1)), cscale(d3, s2));
         a[0] = cadd(a[0], cadd(b1, cadd(b2, b3)));
-        a[1] = cadd(r1, i1);
-        a[6] = csub(r1, i1);
-        a[2] = cadd(r2, i2);
-        a[5] = csub(r2, i2);
-        a[3] = cadd(r3, i3);
-        a[4] = csub(r3, i3);
+        a[1] = cadd_mi<INV>(r1, i1);
+        a[6] = csub_mi<INV>(r1, i1);
+        a[2] = cadd_mi<INV>(r2, i2);
+        a[5] = csub_mi<INV>(r2, i2);
+        a[3] = cadd_mi<INV>(r3, i3);
+        a[4] = csub_mi<INV>(r3, i3);
     }
 }
 
