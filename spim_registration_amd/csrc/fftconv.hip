@@ -32,9 +32,20 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     const sd_v2 t = A.xx * B;                                              // (ax bx, ax by)
     return f2_(__builtin_elementwise_fma(A.yy, sd_v2{-B.y, B.x}, t));      // (- ay by, + ay bx)
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return f2_(v2_(a) + v2_(b)); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return f2_(v2_(a) - v2_(b)); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return f2_(v2_(a) * sd_v2{s, s}); }
+// contract(fast): a scale feeding an add (radix-3/5/7 butterflies) may fuse into one
+// v_pk_fma (the build is -ffp-contract=off for the RL pointwise steps)
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+#pragma clang fp contract(fast)
+    return f2_(v2_(a) + v2_(b));
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+#pragma clang fp contract(fast)
+    return f2_(v2_(a) - v2_(b));
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) {
+#pragma clang fp contract(fast)
+    return f2_(v2_(a) * sd_v2{s, s});
+}
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
