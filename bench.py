@@ -181,12 +181,16 @@ def main():
             # algorithmic HBM bytes per launch of each fused pass (DESIGN.md "kernels"); the
             # z pass reads its kernel's stored z-planes: 2cz+1 of Mz when compact
             kz = 8.0 * sess.kernel_planes(0) / M[2]
+            # z pass: reads all Mz planes, writes Mz (fused FFT) or only the nz interior
+            # planes (direct convolution, zpass_mode 2)
+            zw = 8.0 * nz / M[2] if sess.zpass_mode(0) == 2 else 8.0
+            zb = 8.0 + zw + kz
             classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, 16),
-                       ("z_convolve", 0, 0, 16 + kz), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
+                       ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
                        ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 16 + kz)]
-            b_iter = V * ((12 + 2 * wb) * N + (128.0 + 2 * kz) * S)
-            model = (f"V*((12+2w)N + (128+2k)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
-                     f"k = 8*kernel z-planes/Mz = {kz:.3f}")
+            b_iter = V * ((12 + 2 * wb) * N + (96.0 + 2 * zb) * S)
+            model = (f"V*((12+2w)N + (96+2z)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
+                     f"z = z-pass bytes per bin = {zb:.3f} (8 read + {zw:.3f} write + {kz:.3f} kernel)")
         else:
             classes = [("update_pad", 8 + wb, N, 0), ("quotient_pad", wb, N, 0), ("r2c", 0, 0, 0),
                        ("spec_mul", 0, 0, 0), ("c2r", 0, 0, 0), ("halo_exchange", 0, 0, 0),

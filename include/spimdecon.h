@@ -201,6 +201,11 @@ int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3);
 /* z-planes of each stored kernel spectrum (info/bench): 2*cz+1 when the engine
  * keeps compact kernels (the z pass builds their z transform), else Mz */
 int mvd_kernel_planes(mvd_session* h, int slab, int* planes);
+/* z pass of the engine (info/bench): 0 = fused FFT z pass with full kernel
+ * spectra, 1 = fused FFT z pass with compact kernels, 2 = direct circular
+ * convolution with the compact kernel (only the nz interior planes written);
+ * -1 for the rocFFT backend */
+int mvd_zpass_mode(mvd_session* h, int slab, int* mode);
 /* HIP stream the session launches on (hipStream_t as void*) */
 void* mvd_stream(mvd_session* h);
 /* per-kernel timing: when enabled, mvd_run records HIP events around every

@@ -116,6 +116,7 @@ SIGNATURES = {
     "mvd_psi_device": (C.c_void_p, [C.c_void_p, C.c_int]),
     "mvd_fft_dims": (C.c_int, [C.c_void_p, C.c_int, _pi64]),
     "mvd_kernel_planes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "mvd_zpass_mode": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "mvd_stream": (C.c_void_p, [C.c_void_p]),
     "mvd_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "mvd_timing": (C.c_int, [C.c_void_p, _pd]),

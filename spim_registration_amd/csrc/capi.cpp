@@ -263,6 +263,10 @@ int mvd_kernel_planes(mvd_session* h, int slab, int* planes) {
     return guarded([&] { SESSION(h); SD_CHECK(planes, SPIMDECON_ERR_ARG, "null"); *planes = S.kernel_planes(slab); });
 }
 
+int mvd_zpass_mode(mvd_session* h, int slab, int* mode) {
+    return guarded([&] { SESSION(h); SD_CHECK(mode, SPIMDECON_ERR_ARG, "null"); *mode = S.zpass_mode(slab); });
+}
+
 void* mvd_stream(mvd_session* h) {
     void* r = nullptr;
     guarded([&] { SESSION(h); r = S.stream(); });

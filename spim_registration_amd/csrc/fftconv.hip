@@ -472,6 +472,7 @@ constexpr int kCThreads = 1024;
 #include "fftconv_2f.inc"
 #include "fftconv_x.inc"
 #include "fftconv_xt.inc"
+#include "fftconv_zd.inc"
 
 // ------------------------------------------------------------------ host side
 
@@ -870,7 +871,8 @@ void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx,
     // x and y transforms of the placed kernel (work = full spectrum buffer), then the
     // z-planes qz in [-kc, kc] (wrapped) -> Kc[qz + kc]: all the z pass needs, since
     // the placed kernel is zero outside them (|qz| <= kz/2 <= cz)
-    SD_CHECK(engine_kernel_compact_ok(p), SPIMDECON_ERR_ARG, "compact kernel path not available");
+    SD_CHECK(engine_kernel_compact_ok(p) || engine_zdirect_ok(p), SPIMDECON_ERR_ARG,
+             "compact kernel path not available");
     SD_CHECK(kz / 2 <= p.g.cz, SPIMDECON_ERR_ARG, "kernel z half size exceeds the halo");
     XArgs a = base_args(p);
     a.Cout = work;
@@ -895,7 +897,64 @@ void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx,
     SD_HIP(hipStreamSynchronize(s));
 }
 
+// direct z convolution (fftconv_zd.inc): SPIMDECON_ZDIRECT=0 selects the fused FFT
+// z pass (k_col2f MODE 5) instead, for A/B runs and tests
+static bool zdirect_enabled() {
+    const char* e = std::getenv("SPIMDECON_ZDIRECT");  // read per call (tests toggle it)
+    return !(e && e[0] == '0');
+}
+
+// taps bound KC: 4 or 8.  Measured at 540^3 against the fused FFT z pass (0.30 ms):
+// kc 4 0.258, kc 6 0.272, kc 8 0.274 ms; kc 12 (25 taps) 0.437 ms with KC = 12 (the
+// taps no longer fit the registers beside the accumulators), so larger kernels keep
+// the FFT z pass
+static int zdirect_kc_bound(int kc) {
+    for (int b : {4, 8})
+        if (kc <= b) return b;
+    return 0;
+}
+
+static size_t zdirect_lds(const SpectralPlan& p, int KC) {
+    return size_t((p.g.Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
+}
+
+bool engine_zdirect_ok(const SpectralPlan& p) {
+    const int KC = zdirect_kc_bound(p.g.cz);
+    return zdirect_enabled() && KC > 0 && p.Hp % kZdTX == 0 && KC <= p.g.Mz &&
+           zdirect_lds(p, KC) <= 160 * 1024 &&
+           uint64_t(p.spectrum_elems()) * sizeof(float2) < (uint64_t(1) << 31);
+}
+
+int engine_zpass_mode(const SpectralPlan& p, bool compact) {
+    if (!compact) return 0;
+    return engine_zdirect_ok(p) ? 2 : 1;
+}
+
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
+    if (engine_zdirect_ok(p)) {
+        const int KC = zdirect_kc_bound(p.g.cz);
+        const size_t lds = zdirect_lds(p, KC);
+        const int64_t ntiles = (p.Hp / kZdTX) * p.g.My;
+        const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
+        const uint32_t bytes = uint32_t(uint64_t(p.spectrum_elems()) * sizeof(float2));
+        const uint32_t kbytes = uint32_t(uint64_t(engine_kernel_compact_elems(p)) * sizeof(float2));
+        const float kscale = float(p.g.Mz);
+        bool done = false;
+#define SD_ZD(KCV)                                                                                   \
+        if (!done && KC == (KCV)) {                                                                  \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdirect<KCV, 8>),           \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));       \
+            hipLaunchKernelGGL((k_zdirect<KCV, 8>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, \
+                               C, Kc, p.g.cz, bytes, kbytes, kscale);                                \
+            done = true;                                                                             \
+        }
+        SD_ZD(4) SD_ZD(8)
+#undef SD_ZD
+        SD_CHECK(done, SPIMDECON_ERR_ARG, "no direct z kernel for this kernel size");
+        SD_HIP(hipGetLastError());
+        return;
+    }
     const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz);
     SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
 }

@@ -69,6 +69,11 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
 // (engine_zpass_compact) computes the z transform in its tiles.  `work` is a
 // full spectrum_elems() scratch buffer.
 bool engine_kernel_compact_ok(const SpectralPlan& p);
+// the direct z convolution (fftconv_zd.inc) applies: compact kernels then run it
+bool engine_zdirect_ok(const SpectralPlan& p);
+// z pass of a slab: 0 = fused FFT with full kernel spectra, 1 = fused FFT with
+// compact kernels, 2 = direct convolution with compact kernels
+int engine_zpass_mode(const SpectralPlan& p, bool compact);
 int64_t engine_kernel_compact_elems(const SpectralPlan& p);
 void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz, float scale,
                            float2* work, float2* Kc, hipStream_t s);

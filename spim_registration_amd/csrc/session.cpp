@@ -215,7 +215,7 @@ void Session::build_spectra() {
             // SPIMDECON_ZK=full / =reg asks for the full spectra (A/B runs)
             const char* zk = std::getenv("SPIMDECON_ZK");  // read per session (tests toggle it)
             const bool full_k = zk && (zk[0] == 'f' || zk[0] == 'r');
-            sl.kcompact = !full_k && engine_kernel_compact_ok(sl.sp);
+            sl.kcompact = !full_k && (engine_zdirect_ok(sl.sp) || engine_kernel_compact_ok(sl.sp));
             DBuf<float2> work;
             if (sl.kcompact) work.alloc(ne);
             for (int v = 0; v < nviews_; ++v) {
@@ -627,6 +627,13 @@ void Session::fft_dims(int slab, int64_t* out3) const {
     SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
     for (int d = 0; d < 3; ++d) out3[d] = slabs_[slab].pd.M[d];
+}
+
+int Session::zpass_mode(int slab) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
+    if (backend_ != 0) return -1;
+    return engine_zpass_mode(slabs_[slab].sp, slabs_[slab].kcompact);
 }
 
 int Session::kernel_planes(int slab) const {

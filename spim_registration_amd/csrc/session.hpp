@@ -68,6 +68,7 @@ public:
     float* psi_device(int slab);
     void fft_dims(int slab, int64_t* out3) const;
     int kernel_planes(int slab) const;
+    int zpass_mode(int slab) const;
     hipStream_t stream() const { return stream_; }
     void enable_timing(bool on) { timing_on_ = on; }
     void timing(double* out16);

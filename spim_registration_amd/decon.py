@@ -245,6 +245,12 @@ class Session:
         check(self.lib.mvd_kernel_planes(self.h, int(slab), C.byref(out)))
         return out.value
 
+    def zpass_mode(self, slab=0):
+        """0 fused FFT z pass (full kernels), 1 fused FFT (compact), 2 direct z convolution."""
+        out = C.c_int()
+        check(self.lib.mvd_zpass_mode(self.h, int(slab), C.byref(out)))
+        return out.value
+
     def enable_timing(self, on=True):
         check(self.lib.mvd_enable_timing(self.h, int(on)))
 
