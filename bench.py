@@ -181,15 +181,18 @@ def main():
             # algorithmic HBM bytes per launch of each fused pass (DESIGN.md "kernels"); the
             # z pass reads its kernel's stored z-planes: 2cz+1 of Mz when compact
             kz = 8.0 * sess.kernel_planes(0) / M[2]
-            # z pass: reads all Mz planes, writes Mz (fused FFT) or only the nz interior
-            # planes (direct convolution, zpass_mode 2)
-            zw = 8.0 * nz / M[2] if sess.zpass_mode(0) == 2 else 8.0
+            # z pass: reads all Mz planes, writes only the nz interior planes (the x passes
+            # read nothing else back); the inverse y pass transforms those nz planes only,
+            # so a y launch moves 16 S (forward) or 16 S nz/Mz (inverse), as many of each
+            zw = 8.0 * nz / M[2]
             zb = 8.0 + zw + kz
-            classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, 16),
+            yb = 8.0 * (1.0 + nz / M[2])
+            classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
                        ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
                        ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 16 + kz)]
-            b_iter = V * ((12 + 2 * wb) * N + (96.0 + 2 * zb) * S)
-            model = (f"V*((12+2w)N + (96+2z)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
+            b_iter = V * ((12 + 2 * wb) * N + (32.0 + 4 * yb + 2 * zb) * S)
+            model = (f"V*((12+2w)N + (32+4y+2z)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
+                     f"y = mean y-pass bytes per bin = {yb:.3f}, "
                      f"z = z-pass bytes per bin = {zb:.3f} (8 read + {zw:.3f} write + {kz:.3f} kernel)")
         else:
             classes = [("update_pad", 8 + wb, N, 0), ("quotient_pad", wb, N, 0), ("r2c", 0, 0, 0),

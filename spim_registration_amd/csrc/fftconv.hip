@@ -685,7 +685,10 @@ static int col_grid_rounds() {
 // MODE 5: K is the compact kernel (2*kc+1 z-planes, engine_kernel_compact).
 template <int AXIS, int MODE>
 bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s,
-                  int tx0 = 0, int ntxb = -1, int kc = 0) {
+                  int tx0 = 0, int ntxb = -1, int kc = 0, int nout = -1) {
+    // nout: z planes the pass must produce (AXIS 1: planes transformed; AXIS 2 fused
+    // modes: planes stored) -- the RL loop only reads the nz interior planes back
+    if (nout < 0) nout = int(p.g.Mz);
     const int TX = k2fTX;  // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
     const int L = f.L;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
@@ -701,7 +704,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     if (MODE == 5 && (AXIS != 2 || kplanes > f.n2)) return false;
     if (ntxb < 0) ntxb = int(p.Hp / TX);
     SD_CHECK(tx0 >= 0 && ntxb > 0 && tx0 + ntxb <= p.Hp / TX, SPIMDECON_ERR_ARG, "bad column band");
-    const int64_t ntiles = int64_t(ntxb) * (AXIS == 1 ? p.g.Mz : p.g.My);
+    const int64_t ntiles = int64_t(ntxb) * (AXIS == 1 ? nout : p.g.My);
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
     const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
     const int n1 = f.n1, n2 = f.n2;
@@ -713,7 +716,8 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
             SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv>), \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
             hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv>), dim3(grid), dim3(T * TRv), lds, s,     \
-                               p.g, p.Hp, f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes));  \
+                               p.g, p.Hp, f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes), \
+                               nout);                                                              \
             done = true;                                                                                   \
         }                                                                                                  \
     }
@@ -728,15 +732,16 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
 }
 
 template <int AXIS, bool INV, int ZMODE>
-void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s) {
+void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s,
+                int nout = -1) {
     static const bool zk_lds = [] {  // SPIMDECON_ZK=reg: kernel spectrum in phase-B registers (A/B)
         const char* e = std::getenv("SPIMDECON_ZK");
         return !(e && e[0] == 'r');
     }();
     if constexpr (ZMODE == 1) {
-        if (f.n1 && zk_lds && launch_col2f<AXIS, 4>(p, f, C, K, s)) return;
+        if (f.n1 && zk_lds && launch_col2f<AXIS, 4>(p, f, C, K, s, 0, -1, 0, nout)) return;
     }
-    if (f.n1 && launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s)) return;
+    if (f.n1 && launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s, 0, -1, 0, nout)) return;
     const int tx = col_tx(f.L);
     SD_CHECK(f.L * tx / 2 <= kColMaxU * kCThreads, SPIMDECON_ERR_ARG, "column tile exceeds prefetch registers");
     const size_t lds = size_t(2 * f.L * tx + f.L) * sizeof(float2);
@@ -955,19 +960,20 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         SD_HIP(hipGetLastError());
         return;
     }
-    const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz);
+    const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz, int(p.g.nz));
     SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
 }
 
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
-    if (inv) launch_col<1, true, 0>(p, p.fy, C, nullptr, s);
+    // the inverse feeds the x passes, which read the nz interior planes only
+    if (inv) launch_col<1, true, 0>(p, p.fy, C, nullptr, s, int(p.g.nz));
     else launch_col<1, false, 0>(p, p.fy, C, nullptr, s);
 }
 
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s) {
     // fused forward * K * inverse (0.57 ms at 540^3) beat forward z + (C*K) inverse z
     // as two launches (0.61 ms)
-    if (K) launch_col<2, false, 1>(p, p.fz, C, K, s);
+    if (K) launch_col<2, false, 1>(p, p.fz, C, K, s, int(p.g.nz));
     else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
 }
 
