@@ -909,12 +909,12 @@ static bool zdirect_enabled() {
     return !(e && e[0] == '0');
 }
 
-// taps bound KC: 4 or 8.  Measured at 540^3 against the fused FFT z pass (0.30 ms):
-// kc 4 0.258, kc 6 0.272, kc 8 0.274 ms; kc 12 (25 taps) 0.437 ms with KC = 12 (the
-// taps no longer fit the registers beside the accumulators), so larger kernels keep
-// the FFT z pass
+// taps bound KC: 4, 8 or 12.  Measured at 540^3 against the fused FFT z pass
+// (0.30-0.31 ms): kc 4 0.258, kc 6 0.272, kc 8 0.274 ms (8 outputs per thread round);
+// kc 12 (25 taps) 0.298 ms with 4 outputs per round (0.437 with 8: the taps and
+// accumulators spilled).  Larger kernels keep the FFT z pass.
 static int zdirect_kc_bound(int kc) {
-    for (int b : {4, 8})
+    for (int b : {4, 8, 12})
         if (kc <= b) return b;
     return 0;
 }
@@ -955,6 +955,13 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
             done = true;                                                                             \
         }
         SD_ZD(4) SD_ZD(8)
+        if (!done && KC == 12) {  // 4 outputs per thread round: the 25 taps + 4 accumulators fit
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdirect<12, 4>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
+            hipLaunchKernelGGL((k_zdirect<12, 4>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, Kc,
+                               p.g.cz, bytes, kbytes, kscale);
+            done = true;
+        }
 #undef SD_ZD
         SD_CHECK(done, SPIMDECON_ERR_ARG, "no direct z kernel for this kernel size");
         SD_HIP(hipGetLastError());

@@ -211,6 +211,7 @@ def test_no_cpu_device(gpu):
 
 @pytest.mark.parametrize("shape,ksize", [((40, 18, 22), (9, 5, 7)),       # Mz 48 = 6*8
                                          ((520, 10, 12), (3, 3, 17)),     # Mz 540 = 20*27, kc 8
+                                         ((516, 10, 12), (3, 3, 25)),     # Mz 540, kc 12 (4 outputs)
                                          ((100, 16, 14), (5, 7, 15))])    # Mz 128 = 8*16
 def test_compact_kernel_z_pass(gpu, shape, ksize, monkeypatch):
     """The two compact-kernel z passes -- the direct circular convolution with the
@@ -239,26 +240,3 @@ def test_compact_kernel_z_pass(gpu, shape, ksize, monkeypatch):
     res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
     assert rel_l2(out[0], res.psi) < TOL
 
-
-def test_compact_fft_z_pass_default_for_25_plane_kernels(gpu, monkeypatch):
-    """25-plane kernels (kc 12) keep the fused FFT z pass with compact kernels (the
-    direct convolution is for kc <= 8); it agrees with the full kernel spectra."""
-    shape, ksize = (516, 10, 12), (3, 3, 25)   # Mz 540 = 20*27
-    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
-    out = []
-    for zk, mode in (("compact", 1), ("full", 0)):
-        monkeypatch.setenv("SPIMDECON_ZK", zk)
-        monkeypatch.delenv("SPIMDECON_ZDIRECT", raising=False)
-        with Session(shape[::-1], fft_pad_policy="fast") as s:
-            for i, w, k in zip(imgs, ws, ks):
-                s.add_view(i, w, k)
-            s.init(PSFTYPE.OPTIMIZATION_I)
-            assert s.zpass_mode() == mode
-            s.init_psi()
-            s.run(3, 0.006)
-            s.apply_mask()
-            out.append(s.get_psi())
-    assert not np.array_equal(out[0], out[1])
-    assert rel_l2(out[0], out[1]) < 1e-5
-    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
-    assert rel_l2(out[0], res.psi) < TOL
