@@ -790,7 +790,7 @@ int64_t engine_fast_size(int64_t need, bool even, int policy) {
     return fast * 4 <= smooth * 5 ? fast : smooth;
 }
 
-void SpectralPlan::create(const SlabGeom& geom, bool allow_2f) {
+void SpectralPlan::create(const SlabGeom& geom, bool allow_2f, bool z_fft) {
     g = geom;
     SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");
     Hx = g.Mx / 2 + 1;
@@ -798,7 +798,12 @@ void SpectralPlan::create(const SlabGeom& geom, bool allow_2f) {
     hipStream_t s = nullptr;
     fx = make_fft(int(g.Mx), allow_2f, twx, s);
     fy = make_fft(int(g.My), allow_2f, twy, s);
-    fz = make_fft(int(g.Mz), allow_2f, twz, s);
+    if (z_fft) {
+        fz = make_fft(int(g.Mz), allow_2f, twz, s);
+    } else {
+        fz = Fft1D{};
+        fz.L = int(g.Mz);
+    }
     const int64_t nrows = g.My * g.Mz;
     std::vector<int> rm(nrows), ro(nrows);
     auto mir = [](int64_t sidx, int64_t n) -> int64_t {
@@ -923,11 +928,16 @@ static size_t zdirect_lds(const SpectralPlan& p, int KC) {
     return size_t((p.g.Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
 }
 
+bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
+    const int KC = zdirect_kc_bound(cz);
+    const int64_t Hp = ceil_div(Mx / 2 + 1, int64_t(16)) * 16;
+    const size_t lds = size_t((Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
+    return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && lds <= 160 * 1024 &&
+           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) < (uint64_t(1) << 31);
+}
+
 bool engine_zdirect_ok(const SpectralPlan& p) {
-    const int KC = zdirect_kc_bound(p.g.cz);
-    return zdirect_enabled() && KC > 0 && p.Hp % kZdTX == 0 && KC <= p.g.Mz &&
-           zdirect_lds(p, KC) <= 160 * 1024 &&
-           uint64_t(p.spectrum_elems()) * sizeof(float2) < (uint64_t(1) << 31);
+    return p.Hp % kZdTX == 0 && engine_zdirect_dims_ok(p.g.Mx, p.g.My, p.g.Mz, p.g.cz);
 }
 
 int engine_zpass_mode(const SpectralPlan& p, bool compact) {

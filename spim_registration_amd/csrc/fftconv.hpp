@@ -49,7 +49,9 @@ struct SpectralPlan {
     DBuf<int> row_one;     // [My*Mz] own local row if interior; -2 constant 1; -1 skip
     int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
     // allow_2f: use the two-factor register kernels for lengths in the fast-path table
-    void create(const SlabGeom& geom, bool allow_2f);
+    // z_fft = false: no z transform plan (the direct z convolution needs none, and then
+    // Mz = nz + 2 cz need not be an FFT length)
+    void create(const SlabGeom& geom, bool allow_2f, bool z_fft = true);
 };
 
 // FFT length for `need` samples (even when `even`).  policy 0: the two-factor
@@ -71,6 +73,9 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
 bool engine_kernel_compact_ok(const SpectralPlan& p);
 // the direct z convolution (fftconv_zd.inc) applies: compact kernels then run it
 bool engine_zdirect_ok(const SpectralPlan& p);
+// the same decision from the padded dims, before a plan exists (the session then
+// sizes Mz = nz + 2 cz exactly)
+bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz);
 // z pass of a slab: 0 = fused FFT with full kernel spectra, 1 = fused FFT with
 // compact kernels, 2 = direct convolution with compact kernels
 int engine_zpass_mode(const SpectralPlan& p, bool compact);

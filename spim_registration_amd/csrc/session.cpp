@@ -168,6 +168,13 @@ void Session::build_spectra() {
         sl.pd.M[0] = engine_fast_size(g.nx + 2 * g.cx, true, pol);
         sl.pd.M[1] = engine_fast_size(g.ny + 2 * g.cy, false, pol);
         sl.pd.M[2] = engine_fast_size(g.nz + 2 * g.cz, false, pol);
+        // the direct z convolution needs no z FFT: Mz = nz + 2 cz exactly (unless the
+        // full kernel spectra are asked for, SPIMDECON_ZK=full/reg)
+        const char* zk = std::getenv("SPIMDECON_ZK");
+        const bool zk_full = zk && (zk[0] == 'f' || zk[0] == 'r');
+        sl.zexact = backend_ == 0 && !zk_full &&
+                    engine_zdirect_dims_ok(sl.pd.M[0], sl.pd.M[1], g.nz + 2 * g.cz, g.cz);
+        if (sl.zexact) sl.pd.M[2] = g.nz + 2 * g.cz;
         g.Mx = sl.pd.M[0];
         g.My = sl.pd.M[1];
         g.Mz = sl.pd.M[2];
@@ -203,7 +210,7 @@ void Session::build_spectra() {
                 }
             }
         } else {
-            sl.sp.create(g, p_.fft_pad_policy != 2);
+            sl.sp.create(g, p_.fft_pad_policy != 2, !sl.zexact);
             const size_t ne = size_t(sl.sp.spectrum_elems());
             sl.C1.alloc(ne);
             sl.C2.alloc(ne);
@@ -216,6 +223,8 @@ void Session::build_spectra() {
             const char* zk = std::getenv("SPIMDECON_ZK");  // read per session (tests toggle it)
             const bool full_k = zk && (zk[0] == 'f' || zk[0] == 'r');
             sl.kcompact = !full_k && (engine_zdirect_ok(sl.sp) || engine_kernel_compact_ok(sl.sp));
+            SD_CHECK(!sl.zexact || (sl.kcompact && engine_zdirect_ok(sl.sp)), SPIMDECON_ERR_STATE,
+                     "exact-Mz slab without the direct z pass");
             DBuf<float2> work;
             if (sl.kcompact) work.alloc(ne);
             for (int v = 0; v < nviews_; ++v) {

@@ -41,6 +41,7 @@ struct SlabState {
     DBuf<float2> C1, C2;
     std::vector<DBuf<float2>> e1spec, e2spec;  // full kernel spectra, or compact ones (kcompact)
     bool kcompact = false;
+    bool zexact = false;  // Mz = nz + 2 cz (direct z pass, no z FFT plan)
     DBuf<double> partials;
     DBuf<const void*> img_ptrs;
     std::unique_ptr<FftPlan3D> fft;

@@ -9,4 +9,5 @@ timeout -k 10 400 python3 bench.py > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.l
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o k --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/kt.log 2>&1 &&
 cp $(ls $OUT/kt/*/k_kernel_stats.csv $OUT/kt/k_kernel_stats.csv 2>/dev/null | head -1) $OUT/kernel_stats.csv &&
 tools/pmc_engine.sh $OUT/pmc &&
-python3 tools/pmc_summary.py $OUT/pmc --json $OUT/pmc_traffic.json --dims 540,540,540 > $OUT/pmc.md
+DIMS=$(python3 -c "import json; print(','.join(map(str, json.load(open('$OUT/bench.json'))['config']['fft_dims_xyz'])))") &&
+python3 tools/pmc_summary.py $OUT/pmc --json $OUT/pmc_traffic.json --dims $DIMS > $OUT/pmc.md
