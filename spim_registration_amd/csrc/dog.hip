@@ -107,6 +107,165 @@ __global__ __launch_bounds__(kBlock) void k_sep_pass(Dims3 d, int axis, const fl
     }
 }
 
+// Tiled separable passes (the bench path): 32-bit indices, the line segment of a
+// block staged in LDS once (extension and normalisation applied while loading),
+// taps from LDS, the same float32 tap order per output as k_sep_pass.  x pass: a
+// block = 256 consecutive outputs of one row; y / z passes: 64 x-columns x 64
+// positions along the axis (lanes run along x: coalesced, conflict-free).
+typedef float dg_v2 __attribute__((ext_vector_type(2)));
+constexpr int kSepX = 256;
+constexpr int kSepTX = 64;
+constexpr int kSepTY = 4;
+constexpr int kSepTL = 64;
+
+__device__ __forceinline__ int ext_index32(int i, int n, int mode, bool& outside) {
+    outside = false;
+    if (i >= 0 && i < n) return i;
+    if (mode == OOB_BORDER) return i < 0 ? 0 : n - 1;
+    if (mode == OOB_MIRROR) {
+        if (n == 1) return 0;
+        const int p = 2 * (n - 1);
+        int j = i % p;
+        if (j < 0) j += p;
+        return j >= n ? p - j : j;
+    }
+    outside = true;
+    return 0;
+}
+
+template <int NK>
+__global__ __launch_bounds__(kSepX) void k_sep_x(Dims3 d, const float* __restrict__ in0,
+                                                  const float* __restrict__ in1, const float* __restrict__ k0,
+                                                  const float* __restrict__ k1, int K, int mode, float value,
+                                                  float* __restrict__ out0, float* __restrict__ out1, int dog_out,
+                                                  float dog_scale, const float* mm) {
+    // NK == 2: both kernels' operands interleaved (float2), so one packed v_pk_mul /
+    // v_pk_add (IEEE round-to-nearest per component, no FMA: bit-exact) serves both
+    extern __shared__ __attribute__((aligned(8))) float sm[];
+    const int r = K / 2;
+    const int W = kSepX + K - 1;
+    float* s0 = sm;                 // NK == 1: [W]; NK == 2: float2 [W]
+    float* t0 = sm + NK * W;        // NK == 1: [K]; NK == 2: float2 [K]
+    float2* s01 = reinterpret_cast<float2*>(sm);
+    float2* t01 = reinterpret_cast<float2*>(t0);
+    const int nx = int(d.nx);
+    const int x0 = int(blockIdx.x) * kSepX;
+    const uint32_t row = (uint32_t(blockIdx.z) * uint32_t(d.ny) + blockIdx.y) * uint32_t(nx);
+    const int t = threadIdx.x;
+    for (int i = t; i < K; i += kSepX) {
+        if (NK == 2) t01[i] = make_float2(k0[i], k1[i]);
+        else t0[i] = k0[i];
+    }
+    const bool same = in1 == nullptr || in1 == in0;
+    for (int i = t; i < W; i += kSepX) {
+        bool outside;
+        const int src = ext_index32(x0 - r + i, nx, mode, outside);
+        float v0, v1;
+        if (outside) {
+            v0 = mode == OOB_VALUE ? value : 0.0f;
+            v1 = v0;
+        } else {
+            v0 = normalize(in0[row + src], mm);
+            v1 = same ? v0 : normalize(in1[row + src], mm);
+        }
+        if (NK == 2) s01[i] = make_float2(v0, v1);
+        else s0[i] = v0;
+    }
+    __syncthreads();
+    const int x = x0 + t;
+    if (x >= nx) return;
+    float a0 = 0.0f, a1 = 0.0f;
+    if constexpr (NK == 2) {
+        dg_v2 acc = {0.0f, 0.0f};
+        for (int j = 0; j < K; ++j) {
+            const float2 v = s01[t + j], k = t01[j];
+            acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};  // tap order kept, no contraction
+        }
+        a0 = acc.x;
+        a1 = acc.y;
+    } else {
+        for (int j = 0; j < K; ++j) a0 = __fadd_rn(a0, __fmul_rn(s0[t + j], t0[j]));
+    }
+    if (dog_out) {
+        out0[row + x] = __fmul_rn(__fsub_rn(a1, a0), dog_scale);
+    } else {
+        out0[row + x] = a0;
+        if (NK == 2) out1[row + x] = a1;
+    }
+}
+
+// AX 1 (y) or 2 (z): grid (x tiles, axis tiles, other coordinate)
+template <int NK, int AX>
+__global__ __launch_bounds__(kSepTX * kSepTY) void k_sep_yz(Dims3 d, const float* __restrict__ in0,
+                                                            const float* __restrict__ in1,
+                                                            const float* __restrict__ k0,
+                                                            const float* __restrict__ k1, int K, int mode,
+                                                            float value, float* __restrict__ out0,
+                                                            float* __restrict__ out1, int dog_out,
+                                                            float dog_scale, const float* mm) {
+    extern __shared__ __attribute__((aligned(8))) float sm[];
+    const int r = K / 2;
+    const int H = kSepTL + K - 1;  // staged positions along the axis
+    float* s0 = sm;                       // NK == 1: [H][64]; NK == 2: float2 [H][64]
+    float* t0 = sm + NK * H * kSepTX;     // NK == 1: [K]; NK == 2: float2 [K]
+    float2* s01 = reinterpret_cast<float2*>(sm);
+    float2* t01 = reinterpret_cast<float2*>(t0);
+    const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
+    const int len = AX == 1 ? ny : nz;
+    const uint32_t astride = AX == 1 ? uint32_t(nx) : uint32_t(nx) * uint32_t(ny);
+    const int tx = threadIdx.x % kSepTX, ty = threadIdx.x / kSepTX;
+    const int x = int(blockIdx.x) * kSepTX + tx;
+    const int a0p = int(blockIdx.y) * kSepTL;
+    const int other = int(blockIdx.z);  // z for the y pass, y for the z pass
+    const uint32_t base = AX == 1 ? uint32_t(other) * uint32_t(nx) * uint32_t(ny) + uint32_t(x)
+                                  : uint32_t(other) * uint32_t(nx) + uint32_t(x);
+    for (int i = threadIdx.x; i < K; i += kSepTX * kSepTY) {
+        if (NK == 2) t01[i] = make_float2(k0[i], k1[i]);
+        else t0[i] = k0[i];
+    }
+    const bool xin = x < nx;
+    const bool same = in1 == nullptr || in1 == in0;
+    for (int i = ty; i < H; i += kSepTY) {
+        bool outside;
+        const int src = ext_index32(a0p - r + i, len, mode, outside);
+        float v0 = 0.0f, v1 = 0.0f;
+        if (outside) {
+            v0 = mode == OOB_VALUE ? value : 0.0f;
+            v1 = v0;
+        } else if (xin) {
+            v0 = normalize(in0[base + uint32_t(src) * astride], mm);
+            v1 = same ? v0 : normalize(in1[base + uint32_t(src) * astride], mm);
+        }
+        if (NK == 2) s01[i * kSepTX + tx] = make_float2(v0, v1);
+        else s0[i * kSepTX + tx] = v0;
+    }
+    __syncthreads();
+    if (!xin) return;
+    for (int o = ty; o < kSepTL; o += kSepTY) {
+        const int p = a0p + o;
+        if (p >= len) break;
+        float a0 = 0.0f, a1 = 0.0f;
+        if constexpr (NK == 2) {
+            dg_v2 acc = {0.0f, 0.0f};
+            for (int j = 0; j < K; ++j) {
+                const float2 v = s01[(o + j) * kSepTX + tx], k = t01[j];
+                acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
+            }
+            a0 = acc.x;
+            a1 = acc.y;
+        } else {
+            for (int j = 0; j < K; ++j) a0 = __fadd_rn(a0, __fmul_rn(s0[(o + j) * kSepTX + tx], t0[j]));
+        }
+        const uint32_t idx = base + uint32_t(p) * astride;
+        if (dog_out) {
+            out0[idx] = __fmul_rn(__fsub_rn(a1, a0), dog_scale);
+        } else {
+            out0[idx] = a0;
+            if (NK == 2) out1[idx] = a1;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in, int64_t n,
                                                     float* __restrict__ partial) {
     __shared__ float smn[kBlock / 64], smx[kBlock / 64];
@@ -172,6 +331,22 @@ __device__ __forceinline__ int special_point(const float* __restrict__ dog, Dims
 
 constexpr int kItems = 16;  // voxels per thread per chunk; chunk = kBlock * kItems
 
+// (x, y, z) of flat index i: 32-bit divisions when the volume allows (a 64-bit
+// division is a ~100-instruction software routine on the GPU)
+__device__ __forceinline__ void flat_coords(int64_t i, const Dims3& d, int64_t& x, int64_t& y, int64_t& z) {
+    if (d.nx * d.ny * d.nz < (int64_t(1) << 32)) {
+        const uint32_t ii = uint32_t(i), nx = uint32_t(d.nx), ny = uint32_t(d.ny);
+        const uint32_t q = ii / nx;
+        x = ii - q * nx;
+        z = q / ny;
+        y = q - uint32_t(z) * ny;
+    } else {
+        x = i % d.nx;
+        y = (i / d.nx) % d.ny;
+        z = i / (d.nx * d.ny);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_peaks_count(const float* __restrict__ dog, Dims3 d,
                                                          float minv, int want_min, int want_max,
                                                          int* __restrict__ counts) {
@@ -182,7 +357,8 @@ __global__ __launch_bounds__(kBlock) void k_peaks_count(const float* __restrict_
     for (int it = 0; it < kItems; ++it) {
         const int64_t i = chunk0 + int64_t(it) * kBlock + threadIdx.x;
         if (i >= n) break;
-        const int64_t x = i % d.nx, y = (i / d.nx) % d.ny, z = i / (d.nx * d.ny);
+        int64_t x, y, z;
+        flat_coords(i, d, x, y, z);
         float v;
         const int sp = special_point(dog, d, i, x, y, z, minv, v);
         cnt += (sp == 2 && want_max) || (sp == 1 && want_min);
@@ -197,15 +373,31 @@ __global__ __launch_bounds__(kBlock) void k_peaks_count(const float* __restrict_
     }
 }
 
-// exclusive scan of counts (single block, sequential per thread chunk)
-__global__ void k_scan(const int* __restrict__ counts, int64_t nb, int64_t* __restrict__ offsets) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    int64_t s = 0;
-    for (int64_t b = 0; b < nb; ++b) {
-        offsets[b] = s;
-        s += counts[b];
+// exclusive scan of counts: one block of kScanThreads, each thread scans a contiguous
+// run of counts sequentially after a block-wide scan of the run totals
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_scan(const int* __restrict__ counts, int64_t nb,
+                                                       int64_t* __restrict__ offsets) {
+    __shared__ int64_t tot[kScanThreads];
+    const int t = threadIdx.x;
+    const int64_t per = (nb + kScanThreads - 1) / kScanThreads;
+    const int64_t b0 = min(nb, int64_t(t) * per), b1 = min(nb, b0 + per);
+    int64_t sum = 0;
+    for (int64_t b = b0; b < b1; ++b) sum += counts[b];
+    tot[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) {  // Hillis-Steele inclusive scan
+        const int64_t v = t >= off ? tot[t - off] : 0;
+        __syncthreads();
+        tot[t] += v;
+        __syncthreads();
     }
-    offsets[nb] = s;
+    int64_t run = tot[t] - sum;  // exclusive prefix of this run
+    for (int64_t b = b0; b < b1; ++b) {
+        offsets[b] = run;
+        run += counts[b];
+    }
+    if (t == kScanThreads - 1) offsets[nb] = tot[t];
 }
 
 struct PeakOut {
@@ -231,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_peaks_write(const float* __restrict_
         float v = 0.0f;
         int64_t x = 0, y = 0, z = 0;
         if (i < n) {
-            x = i % d.nx; y = (i / d.nx) % d.ny; z = i / (d.nx * d.ny);
+            flat_coords(i, d, x, y, z);
             sp = special_point(dog, d, i, x, y, z, minv, v);
         }
         const bool flag = (sp == 2 && want_max) || (sp == 1 && want_min);
@@ -268,6 +460,38 @@ void sep_pass(const Dims3& d, int axis, const float* in0, const float* in1, cons
               const float* k1, int K, int mode, float value, float* out0, float* out1, bool dog,
               float dog_scale, const float* mm, hipStream_t s) {
     const int64_t n = d.nx * d.ny * d.nz;
+    const bool two = in1 || k1;
+    const int nk = two ? 2 : 1;
+    // tiled passes: 32-bit indices, grid y/z extents within 65535
+    const int64_t tl = axis == 0 ? 1 : ceil_div(axis == 1 ? d.ny : d.nz, int64_t(kSepTL));
+    const int64_t oth = axis == 0 ? d.nz : (axis == 1 ? d.nz : d.ny);
+    if (n < (int64_t(1) << 31) && (axis == 0 ? d.ny : tl) <= 65535 && oth <= 65535) {
+        if (axis == 0) {
+            const size_t lds = size_t(nk * (kSepX + K - 1) + nk * K) * sizeof(float);
+            const dim3 grid(unsigned(ceil_div(d.nx, int64_t(kSepX))), unsigned(d.ny), unsigned(d.nz));
+            if (two)
+                hipLaunchKernelGGL(k_sep_x<2>, grid, dim3(kSepX), lds, s, d, in0, in1, k0, k1, K, mode, value,
+                                   out0, out1, int(dog), dog_scale, mm);
+            else
+                hipLaunchKernelGGL(k_sep_x<1>, grid, dim3(kSepX), lds, s, d, in0, in1, k0, k1, K, mode, value,
+                                   out0, out1, int(dog), dog_scale, mm);
+        } else {
+            const size_t lds = size_t(nk * (kSepTL + K - 1) * kSepTX + nk * K) * sizeof(float);
+            const dim3 grid(unsigned(ceil_div(d.nx, int64_t(kSepTX))), unsigned(tl), unsigned(oth));
+#define SD_SEPYZ(NKV, AXV)                                                                              \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_yz<NKV, AXV>),              \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
+            hipLaunchKernelGGL((k_sep_yz<NKV, AXV>), grid, dim3(kSepTX * kSepTY), lds, s, d, in0, in1, k0, \
+                               k1, K, mode, value, out0, out1, int(dog), dog_scale, mm);
+            if (two && axis == 1) { SD_SEPYZ(2, 1) }
+            else if (two) { SD_SEPYZ(2, 2) }
+            else if (axis == 1) { SD_SEPYZ(1, 1) }
+            else { SD_SEPYZ(1, 2) }
+#undef SD_SEPYZ
+        }
+        SD_HIP(hipGetLastError());
+        return;
+    }
     if (in1 || k1)
         hipLaunchKernelGGL(k_sep_pass<2>, dim3(grid_of(n)), dim3(kBlock), 0, s, d, axis, in0, in1, k0,
                            k1, K, mode, value, out0, out1, int(dog), dog_scale, mm);
@@ -535,7 +759,7 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     const int wmin = p->find_min ? 1 : 0, wmax = p->find_max ? 1 : 0;
     hipLaunchKernelGGL(k_peaks_count, dim3(unsigned(nb)), dim3(kBlock), 0, s, dog, d, min_peak, wmin,
                        wmax, counts.p);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(64), 0, s, counts.p, nb, offsets.p);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, counts.p, nb, offsets.p);
     SD_HIP(hipGetLastError());
     int64_t total = 0;
     SD_HIP(hipMemcpyAsync(&total, offsets.p + nb, 8, hipMemcpyDeviceToHost, s));
