@@ -52,16 +52,18 @@ def test_device_query(gpu):
     assert f.getMemDeviceCUDA(-1) == -1          # invalid device -> error, no CPU emulation
 
 
+@pytest.mark.parametrize("sigmas", [[1.7, 2.0, 1.2],     # 15-tap kernels
+                                    [6.0, 3.0, 9.5]])    # 63-tap kernels: halos wider than the image
 @pytest.mark.parametrize("oob", [legacy.OutOfBounds.ZERO, legacy.OutOfBounds.VALUE,
                                  legacy.OutOfBounds.EXTEND_BORDER_PIXELS, legacy.OutOfBounds.MIRROR_SINGLE])
-def test_separable_convolve_n(gpu, oob):
+def test_separable_convolve_n(gpu, oob, sigmas):
     rng = np.random.default_rng(3)
     img = rng.random((13, 17, 19)).astype(np.float32)
     cuda = legacy.CUDASeparableConvolution()
     im = img.copy().reshape(-1)
-    ok = legacy.gauss(im, [19, 17, 13], [1.7, 2.0, 1.2], oob, 0.25, cuda, 0)
+    ok = legacy.gauss(im, [19, 17, 13], sigmas, oob, 0.25, cuda, 0)
     assert ok
-    ks = legacy.get_cuda_kernels([1.7, 2.0, 1.2])
+    ks = legacy.get_cuda_kernels(sigmas)
     mode = {0: "zero", 1: "value", 2: "border", 3: "mirror"}[int(oob)]
     exp = dog_ref.gauss3d(img, ks, mode, 0.25)
     np.testing.assert_array_equal(im.reshape(img.shape), exp)
