@@ -252,7 +252,8 @@ typedef struct spim_interest_point {
 void spim_dog_params_default(spim_dog_params* p);
 
 /* img: dims {nx, ny, nz} x-fastest (not modified).  dog_out (optional, may be
- * NULL) receives the DoG image.  peaks: capacity max_peaks, *npeaks = total
+ * NULL) receives the DoG image.  img and dog_out may be host or device (HIP)
+ * pointers: a view already resident in HBM is not staged through the host.  peaks: capacity max_peaks, *npeaks = total
  * found (may exceed max_peaks: then only max_peaks were written).  These are
  * the DoG extrema with |v| >= threshold (localization 0) or threshold / 10
  * (localization 1), i.e. DifferenceOfGaussianNewPeakFinder.getSimplePeaks. */

@@ -727,7 +727,8 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     auto kp = [&](int axis, int which) { return dk.p + (2 * axis + which) * K; };
 
     DBuf<float> b0(n), b1(n), b2(n), b3(n);
-    SD_HIP(hipMemcpyAsync(b0.p, img, n * 4, hipMemcpyHostToDevice, s));
+    // img / dog_out may be host or device pointers (unified addressing infers the copy)
+    SD_HIP(hipMemcpyAsync(b0.p, img, n * 4, hipMemcpyDefault, s));
     DBuf<float> mm(2 * 4096);
     const bool use_given = !(std::isnan(p->min_intensity) || std::isnan(p->max_intensity) ||
                              std::isinf(p->min_intensity) || std::isinf(p->max_intensity) ||
@@ -749,7 +750,7 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     sep_pass(d, 2, b3.p, b0.p, kp(2, 0), kp(2, 1), K, OOB_MIRROR, 0.f, b1.p, nullptr, true, kinv,
              nullptr, s);
     const float* dog = b1.p;
-    if (dog_out) SD_HIP(hipMemcpyAsync(dog_out, dog, n * 4, hipMemcpyDeviceToHost, s));
+    if (dog_out) SD_HIP(hipMemcpyAsync(dog_out, dog, n * 4, hipMemcpyDefault, s));
 
     // peaks: order-preserving compaction in flat order
     const int64_t chunk = int64_t(kBlock) * kItems;
