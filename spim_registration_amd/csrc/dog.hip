@@ -114,6 +114,7 @@ __global__ __launch_bounds__(kBlock) void k_sep_pass(Dims3 d, int axis, const fl
 // positions along the axis (lanes run along x: coalesced, conflict-free).
 typedef float dg_v2 __attribute__((ext_vector_type(2)));
 constexpr int kSepX = 256;
+constexpr int kSepRows = 8;  // rows per x-pass block (one 256-thread block per row segment was launch-bound)
 constexpr int kSepTX = 64;
 constexpr int kSepTY = 4;
 constexpr int kSepTL = 64;
@@ -150,13 +151,17 @@ __global__ __launch_bounds__(kSepX) void k_sep_x(Dims3 d, const float* __restric
     float2* t01 = reinterpret_cast<float2*>(t0);
     const int nx = int(d.nx);
     const int x0 = int(blockIdx.x) * kSepX;
-    const uint32_t row = (uint32_t(blockIdx.z) * uint32_t(d.ny) + blockIdx.y) * uint32_t(nx);
     const int t = threadIdx.x;
     for (int i = t; i < K; i += kSepX) {
         if (NK == 2) t01[i] = make_float2(k0[i], k1[i]);
         else t0[i] = k0[i];
     }
     const bool same = in1 == nullptr || in1 == in0;
+    const int y0 = int(blockIdx.y) * kSepRows;
+    const int y1 = min(int(d.ny), y0 + kSepRows);
+    for (int y = y0; y < y1; ++y) {
+    const uint32_t row = (uint32_t(blockIdx.z) * uint32_t(d.ny) + uint32_t(y)) * uint32_t(nx);
+    __syncthreads();  // the previous row's LDS reads are done
     for (int i = t; i < W; i += kSepX) {
         bool outside;
         const int src = ext_index32(x0 - r + i, nx, mode, outside);
@@ -173,24 +178,26 @@ __global__ __launch_bounds__(kSepX) void k_sep_x(Dims3 d, const float* __restric
     }
     __syncthreads();
     const int x = x0 + t;
-    if (x >= nx) return;
-    float a0 = 0.0f, a1 = 0.0f;
-    if constexpr (NK == 2) {
-        dg_v2 acc = {0.0f, 0.0f};
-        for (int j = 0; j < K; ++j) {
-            const float2 v = s01[t + j], k = t01[j];
-            acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};  // tap order kept, no contraction
+    if (x < nx) {
+        float a0 = 0.0f, a1 = 0.0f;
+        if constexpr (NK == 2) {
+            dg_v2 acc = {0.0f, 0.0f};
+            for (int j = 0; j < K; ++j) {
+                const float2 v = s01[t + j], k = t01[j];
+                acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};  // tap order kept, no contraction
+            }
+            a0 = acc.x;
+            a1 = acc.y;
+        } else {
+            for (int j = 0; j < K; ++j) a0 = __fadd_rn(a0, __fmul_rn(s0[t + j], t0[j]));
         }
-        a0 = acc.x;
-        a1 = acc.y;
-    } else {
-        for (int j = 0; j < K; ++j) a0 = __fadd_rn(a0, __fmul_rn(s0[t + j], t0[j]));
+        if (dog_out) {
+            out0[row + x] = __fmul_rn(__fsub_rn(a1, a0), dog_scale);
+        } else {
+            out0[row + x] = a0;
+            if (NK == 2) out1[row + x] = a1;
+        }
     }
-    if (dog_out) {
-        out0[row + x] = __fmul_rn(__fsub_rn(a1, a0), dog_scale);
-    } else {
-        out0[row + x] = a0;
-        if (NK == 2) out1[row + x] = a1;
     }
 }
 
@@ -468,7 +475,8 @@ void sep_pass(const Dims3& d, int axis, const float* in0, const float* in1, cons
     if (n < (int64_t(1) << 31) && (axis == 0 ? d.ny : tl) <= 65535 && oth <= 65535) {
         if (axis == 0) {
             const size_t lds = size_t(nk * (kSepX + K - 1) + nk * K) * sizeof(float);
-            const dim3 grid(unsigned(ceil_div(d.nx, int64_t(kSepX))), unsigned(d.ny), unsigned(d.nz));
+            const dim3 grid(unsigned(ceil_div(d.nx, int64_t(kSepX))), unsigned(ceil_div(d.ny, int64_t(kSepRows))),
+                            unsigned(d.nz));
             if (two)
                 hipLaunchKernelGGL(k_sep_x<2>, grid, dim3(kSepX), lds, s, d, in0, in1, k0, k1, K, mode, value,
                                    out0, out1, int(dog), dog_scale, mm);
