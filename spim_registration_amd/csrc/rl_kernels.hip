@@ -196,13 +196,15 @@ __global__ __launch_bounds__(kBlock) void k_update_pad(SlabGeom g, const float* 
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_reduce_partials(const double* __restrict__ partials,
-                                                             int64_t n, double* out, int accumulate) {
-    __shared__ double sh_sum[kWaves];
-    __shared__ float sh_max_unused[kWaves];
-    __shared__ double sh_max[kWaves];
+// one block of kRedThreads: the update pass leaves one {sum, max} per block (one
+// tile per block: ~18 k partials at 540^3), summed in a fixed order (deterministic)
+constexpr int kRedThreads = 1024;
+__global__ __launch_bounds__(kRedThreads) void k_reduce_partials(const double* __restrict__ partials,
+                                                                 int64_t n, double* out, int accumulate) {
+    __shared__ double sh_sum[kRedThreads / 64];
+    __shared__ double sh_max[kRedThreads / 64];
     double sum = 0.0, mx = -1.0;
-    for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    for (int64_t i = threadIdx.x; i < n; i += kRedThreads) {
         sum += partials[2 * i];
         mx = fmax(mx, partials[2 * i + 1]);
     }
@@ -215,10 +217,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_partials(const double* __rest
         sh_sum[wid] = sum;
         sh_max[wid] = mx;
     }
-    (void)sh_max_unused;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w2 = 1; w2 < kWaves; ++w2) {
+        for (int w2 = 1; w2 < kRedThreads / 64; ++w2) {
             sum += sh_sum[w2];
             mx = fmax(mx, sh_max[w2]);
         }
@@ -383,7 +384,7 @@ int64_t launch_update_pad(const SlabGeom& g, Store st, const float* psi_in, cons
 
 void launch_reduce_partials(const double* partials, int64_t nblocks, double* out, int accumulate,
                             hipStream_t s) {
-    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, s, partials, nblocks, out,
+    hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRedThreads), 0, s, partials, nblocks, out,
                        accumulate);
     SD_HIP(hipGetLastError());
 }
