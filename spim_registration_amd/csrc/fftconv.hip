@@ -642,8 +642,10 @@ unsigned launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream
 // launches the x pass; returns its grid (= number of stats partials of an update pass)
 template <int MODE>
 unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
-    if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
+    if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE || MODE == XM_PSI) {
         if (const unsigned gt = launch_xtile<MODE>(a, st, p, s)) return gt;
+    }
+    if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
         if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) return gr;
     }
     const size_t lds = x_lds(p);
