@@ -302,15 +302,22 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in,
     }
 }
 
-__global__ void k_minmax_final(float* partial, int nb) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// min / max over the per-block partials: one wave, lane-strided then shuffles
+// (min and max are order-independent, so the result equals a sequential scan)
+__global__ __launch_bounds__(64) void k_minmax_final(float* partial, int nb) {
     float mn = INFINITY, mx = -INFINITY;
-    for (int b = 0; b < nb; ++b) {
+    for (int b = threadIdx.x; b < nb; b += 64) {
         mn = fminf(mn, partial[2 * b]);
         mx = fmaxf(mx, partial[2 * b + 1]);
     }
-    partial[0] = mn;
-    partial[1] = mx;
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, off, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    }
+    if (threadIdx.x == 0) {
+        partial[0] = mn;
+        partial[1] = mx;
+    }
 }
 
 // InteractiveIntegral.isSpecialPoint: 0 invalid, 1 MIN, 2 MAX
