@@ -202,7 +202,10 @@ __global__ __launch_bounds__(kSepX) void k_sep_x(Dims3 d, const float* __restric
 }
 
 // AX 1 (y) or 2 (z): grid (x tiles, axis tiles, other coordinate)
-template <int NK, int AX>
+// KW > 0: the tap count K == KW is known at compile time and a thread computes 16
+// consecutive outputs from a register window of 16 + KW - 1 staged values (KW + 15
+// LDS reads instead of 16 * KW); same per-output tap order.
+template <int NK, int AX, int KW = 0>
 __global__ __launch_bounds__(kSepTX * kSepTY) void k_sep_yz(Dims3 d, const float* __restrict__ in0,
                                                             const float* __restrict__ in1,
                                                             const float* __restrict__ k0,
@@ -248,6 +251,59 @@ __global__ __launch_bounds__(kSepTX * kSepTY) void k_sep_yz(Dims3 d, const float
     }
     __syncthreads();
     if (!xin) return;
+    if constexpr (KW > 0) {
+        constexpr int OW = kSepTL / kSepTY;  // 16 consecutive outputs per thread
+        constexpr int WN = OW + KW - 1;
+        const int ob = ty * OW;
+        if constexpr (NK == 2) {
+            dg_v2 acc[OW], w[WN];
+#pragma unroll
+            for (int i = 0; i < WN; ++i) {
+                const float2 v = s01[(ob + i) * kSepTX + tx];
+                w[i] = dg_v2{v.x, v.y};
+            }
+#pragma unroll
+            for (int o = 0; o < OW; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const float2 kk = t01[j];
+                const dg_v2 k = dg_v2{kk.x, kk.y};
+#pragma unroll
+                for (int o = 0; o < OW; ++o) acc[o] = acc[o] + w[o + j] * k;  // tap order kept
+            }
+#pragma unroll
+            for (int o = 0; o < OW; ++o) {
+                const int p = a0p + ob + o;
+                if (p < len) {
+                    const uint32_t idx = base + uint32_t(p) * astride;
+                    if (dog_out) {
+                        out0[idx] = __fmul_rn(__fsub_rn(acc[o].y, acc[o].x), dog_scale);
+                    } else {
+                        out0[idx] = acc[o].x;
+                        out1[idx] = acc[o].y;
+                    }
+                }
+            }
+        } else {
+            float acc[OW], w[WN];
+#pragma unroll
+            for (int i = 0; i < WN; ++i) w[i] = s0[(ob + i) * kSepTX + tx];
+#pragma unroll
+            for (int o = 0; o < OW; ++o) acc[o] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const float k = t0[j];
+#pragma unroll
+                for (int o = 0; o < OW; ++o) acc[o] = __fadd_rn(acc[o], __fmul_rn(w[o + j], k));
+            }
+#pragma unroll
+            for (int o = 0; o < OW; ++o) {
+                const int p = a0p + ob + o;
+                if (p < len) out0[base + uint32_t(p) * astride] = acc[o];
+            }
+        }
+        return;
+    }
     for (int o = ty; o < kSepTL; o += kSepTY) {
         const int p = a0p + o;
         if (p >= len) break;
@@ -493,16 +549,21 @@ void sep_pass(const Dims3& d, int axis, const float* in0, const float* in1, cons
         } else {
             const size_t lds = size_t(nk * (kSepTL + K - 1) * kSepTX + nk * K) * sizeof(float);
             const dim3 grid(unsigned(ceil_div(d.nx, int64_t(kSepTX))), unsigned(tl), unsigned(oth));
-#define SD_SEPYZ(NKV, AXV)                                                                              \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_yz<NKV, AXV>),              \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
-            hipLaunchKernelGGL((k_sep_yz<NKV, AXV>), grid, dim3(kSepTX * kSepTY), lds, s, d, in0, in1, k0, \
+#define SD_SEPYZ1(NKV, AXV, KWV)                                                                          \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_yz<NKV, AXV, KWV>),           \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));            \
+            hipLaunchKernelGGL((k_sep_yz<NKV, AXV, KWV>), grid, dim3(kSepTX * kSepTY), lds, s, d, in0, in1, k0, \
                                k1, K, mode, value, out0, out1, int(dog), dog_scale, mm);
+#define SD_SEPYZ(NKV, AXV)                                    \
+            if (K == 7) { SD_SEPYZ1(NKV, AXV, 7) }            \
+            else if (K == 15) { SD_SEPYZ1(NKV, AXV, 15) }     \
+            else { SD_SEPYZ1(NKV, AXV, 0) }
             if (two && axis == 1) { SD_SEPYZ(2, 1) }
             else if (two) { SD_SEPYZ(2, 2) }
             else if (axis == 1) { SD_SEPYZ(1, 1) }
             else { SD_SEPYZ(1, 2) }
 #undef SD_SEPYZ
+#undef SD_SEPYZ1
         }
         SD_HIP(hipGetLastError());
         return;
