@@ -158,7 +158,20 @@ int mvd_comm_unique_id(char* out128);
 int mvd_slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1);
 
 int  mvd_create(const mvd_params* params, mvd_session** out);
+/* One session over several GPUs of this process -- the reference's
+ * MVDeconFFT(img, weight, kernel, factory, int[] deviceList, ...) driven from one
+ * JVM (MVDeconFFT.java:58-64,91-100,424-446).  params.dims is the whole
+ * (this rank's) volume; it is split into ndev * params.local_slabs z-slabs, slabs
+ * [i*local_slabs, (i+1)*local_slabs) on devs[i] (params.device is ignored).  One
+ * mvd_run drives all devices (one host thread each); halo planes move between
+ * neighbouring devices as peer copies over xGMI.  Device ids may repeat (several
+ * groups on one GPU: the same code path, e.g. for testing).  Needs the engine
+ * backend and nranks == 1. */
+int  mvd_create_devices(const int* devs, int ndev, const mvd_params* params, mvd_session** out);
 void mvd_destroy(mvd_session* h);
+/* devices of the session and the device holding slab s (slabs: ndev * local_slabs) */
+int  mvd_num_devices(mvd_session* h, int* ndev);
+int  mvd_slab_device(mvd_session* h, int slab, int* dev);
 
 /* Adds one view (MVDeconInput.add order).  img/weight: this rank's z-range,
  * dims = params.dims; kernel1: raw (un-normalised) PSF of kdims {kx,ky,kz}.
@@ -206,6 +219,9 @@ int mvd_kernel_planes(mvd_session* h, int slab, int* planes);
  * convolution with the compact kernel (only the nz interior planes written);
  * -1 for the rocFFT backend */
 int mvd_zpass_mode(mvd_session* h, int slab, int* mode);
+/* x pass of the last update launch of slab s (info/tests): 2 = two-factor row-pair
+ * tiles, 1 = per-wave rows, 0 = Stockham rows, -1 = no run yet, -2 = rocFFT backend */
+int mvd_xpass_mode(mvd_session* h, int slab, int* mode);
 /* HIP stream the session launches on (hipStream_t as void*) */
 void* mvd_stream(mvd_session* h);
 /* per-kernel timing: when enabled, mvd_run records HIP events around every

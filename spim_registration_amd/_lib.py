@@ -103,7 +103,10 @@ SIGNATURES = {
     "mvd_comm_unique_id": (C.c_int, [C.c_char_p]),
     "mvd_slab_range": (C.c_int, [_i64, C.c_int, C.c_int, _pi64, _pi64]),
     "mvd_create": (C.c_int, [C.POINTER(MvdParams), C.POINTER(C.c_void_p)]),
+    "mvd_create_devices": (C.c_int, [_pi, C.c_int, C.POINTER(MvdParams), C.POINTER(C.c_void_p)]),
     "mvd_destroy": (None, [C.c_void_p]),
+    "mvd_num_devices": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    "mvd_slab_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "mvd_add_view": (C.c_int, [C.c_void_p, _pf, _pf, _pf, _pi]),
     "mvd_add_view_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, _pf, _pi]),
     "mvd_init": (C.c_int, [C.c_void_p, C.c_int]),
@@ -117,6 +120,7 @@ SIGNATURES = {
     "mvd_fft_dims": (C.c_int, [C.c_void_p, C.c_int, _pi64]),
     "mvd_kernel_planes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "mvd_zpass_mode": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "mvd_xpass_mode": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "mvd_stream": (C.c_void_p, [C.c_void_p]),
     "mvd_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "mvd_timing": (C.c_int, [C.c_void_p, _pd]),

@@ -197,6 +197,22 @@ int mvd_create(const mvd_params* params, mvd_session** out) {
     });
 }
 
+int mvd_create_devices(const int* devs, int ndev, const mvd_params* params, mvd_session** out) {
+    return guarded([&] {
+        SD_CHECK(devs && ndev >= 1 && params && out, SPIMDECON_ERR_ARG, "null argument");
+        *out = nullptr;
+        std::vector<int> dl(devs, devs + ndev);
+        auto* h = new mvd_session{nullptr};
+        try {
+            h->s = new Session(*params, dl);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
 void mvd_destroy(mvd_session* h) {
     if (!h) return;
     guarded([&] { delete h->s; });
@@ -267,10 +283,22 @@ int mvd_zpass_mode(mvd_session* h, int slab, int* mode) {
     return guarded([&] { SESSION(h); SD_CHECK(mode, SPIMDECON_ERR_ARG, "null"); *mode = S.zpass_mode(slab); });
 }
 
+int mvd_xpass_mode(mvd_session* h, int slab, int* mode) {
+    return guarded([&] { SESSION(h); SD_CHECK(mode, SPIMDECON_ERR_ARG, "null"); *mode = S.xpass_mode(slab); });
+}
+
 void* mvd_stream(mvd_session* h) {
     void* r = nullptr;
     guarded([&] { SESSION(h); r = S.stream(); });
     return r;
+}
+
+int mvd_num_devices(mvd_session* h, int* ndev) {
+    return guarded([&] { SESSION(h); SD_CHECK(ndev, SPIMDECON_ERR_ARG, "null"); *ndev = S.ndevices(); });
+}
+
+int mvd_slab_device(mvd_session* h, int slab, int* dev) {
+    return guarded([&] { SESSION(h); SD_CHECK(dev, SPIMDECON_ERR_ARG, "null"); *dev = S.slab_device(slab); });
 }
 
 int mvd_enable_timing(mvd_session* h, int on) {

@@ -643,11 +643,18 @@ unsigned launch_xrows(const XArgs& a, Store st, const SpectralPlan& p, hipStream
 template <int MODE>
 unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
     if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE || MODE == XM_PSI) {
-        if (const unsigned gt = launch_xtile<MODE>(a, st, p, s)) return gt;
+        if (const unsigned gt = launch_xtile<MODE>(a, st, p, s)) {
+            if (MODE == XM_UPDATE) p.xmode_update = 2;
+            return gt;
+        }
     }
     if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
-        if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) return gr;
+        if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) {
+            if (MODE == XM_UPDATE) p.xmode_update = 1;
+            return gr;
+        }
     }
+    if (MODE == XM_UPDATE) p.xmode_update = 0;
     const size_t lds = x_lds(p);
     SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "x pass LDS too large");
     SD_CHECK(p.g.My * p.g.Mz < (int64_t(1) << 30), SPIMDECON_ERR_ARG, "too many rows");
@@ -934,7 +941,9 @@ bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
     const int KC = zdirect_kc_bound(cz);
     const int64_t Hp = ceil_div(Mx / 2 + 1, int64_t(16)) * 16;
     const size_t lds = size_t((Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
-    return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && lds <= 160 * 1024 &&
+    // Mz >= KC: the wrap copies of k_zdirect fill every window slot only then (a
+    // window slot left unwritten would multiply stale LDS by a zero tap: 0 * NaN)
+    return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC && lds <= 160 * 1024 &&
            uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) < (uint64_t(1) << 31);
 }
 

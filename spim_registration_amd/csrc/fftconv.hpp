@@ -47,6 +47,9 @@ struct SpectralPlan {
     DBuf<float2> twx, twy, twz;
     DBuf<int> row_mirror;  // [My*Mz] local source row (lz*ny+ly) of the mirror extension; -1 skip
     DBuf<int> row_one;     // [My*Mz] own local row if interior; -2 constant 1; -1 skip
+    // x pass the last update launch ran: 2 = two-factor tiles (k_xtile), 1 = per-wave
+    // rows (k_xrows), 0 = Stockham rows (k_xpass); -1 = none yet (mvd_xpass_mode)
+    mutable int xmode_update = -1;
     int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
     // allow_2f: use the two-factor register kernels for lengths in the fast-path table
     // z_fft = false: no z transform plan (the direct z convolution needs none, and then

@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 namespace spimdecon {
 
@@ -21,37 +23,85 @@ void slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1) {
     *z1 = *z0 + base + (idx < rem ? 1 : 0);
 }
 
-Session::Session(const mvd_params& p) : p_(p) {
+void HostBarrier::wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (aborted_) fail(SPIMDECON_ERR_STATE, "device group aborted");
+    const uint64_t gen = gen_;
+    if (++count_ == n_) {
+        count_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        return;
+    }
+    cv_.wait(lk, [&] { return gen_ != gen || aborted_; });
+    if (gen_ == gen) fail(SPIMDECON_ERR_STATE, "device group aborted");
+}
+
+void HostBarrier::abort() {
+    std::lock_guard<std::mutex> lk(mu_);
+    aborted_ = true;
+    cv_.notify_all();
+}
+
+Session::Session(const mvd_params& p, const std::vector<int>& devs) : p_(p) {
     SD_CHECK(p.dims[0] >= 1 && p.dims[1] >= 1 && p.dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
     SD_CHECK(p.local_slabs >= 1, SPIMDECON_ERR_ARG, "local_slabs must be >= 1");
-    SD_CHECK(p.local_slabs <= p.dims[2], SPIMDECON_ERR_ARG, "more slabs than z planes");
     SD_CHECK(p.nranks >= 1 && p.rank >= 0 && p.rank < p.nranks, SPIMDECON_ERR_ARG, "bad rank");
     SD_CHECK(p.ij_threads >= 1, SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
+    std::vector<int> dl = devs.empty() ? std::vector<int>{p.device} : devs;
+    const int G = int(dl.size());
+    SD_CHECK(G == 1 || p.nranks == 1, SPIMDECON_ERR_ARG,
+             "several devices per process and several RCCL ranks cannot be combined");
+    SD_CHECK(G == 1 || p.fft_backend == 0, SPIMDECON_ERR_ARG, "several devices need the engine backend");
+    const int nslabs = G * p.local_slabs;
+    SD_CHECK(nslabs <= p.dims[2], SPIMDECON_ERR_ARG, "more slabs than z planes");
     if (p_.nz_global <= 0) p_.nz_global = p.dims[2];
     SD_CHECK(p_.z_offset >= 0 && p_.z_offset + p.dims[2] <= p_.nz_global, SPIMDECON_ERR_ARG,
              "z range outside nz_global");
     SD_CHECK(p_.nranks == 1 || p_.comm_id != nullptr, SPIMDECON_ERR_ARG,
              "nranks > 1 needs comm_id");
-    check_device(p.device);
+    for (int d : dl) check_device(d);
+    p_.device = dl[0];
     store_ = p.storage_fp16 ? Store::F16 : Store::F32;
     backend_ = p.fft_backend;
     SD_CHECK(backend_ == 0 || backend_ == 1, SPIMDECON_ERR_ARG, "unknown fft_backend");
-    DeviceGuard guard(p.device);
-    SD_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    SD_HIP(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking));
-    SD_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
-    SD_HIP(hipEventCreateWithFlags(&ev_x_, hipEventDisableTiming));
+    groups_.resize(G);
+    for (int gi = 0; gi < G; ++gi) {
+        DevGroup& gr = groups_[gi];
+        gr.dev = dl[gi];
+        gr.s0 = gi * p.local_slabs;
+        gr.s1 = gr.s0 + p.local_slabs;
+        DeviceGuard guard(gr.dev);
+        SD_HIP(hipStreamCreateWithFlags(&gr.stream, hipStreamNonBlocking));
+        SD_HIP(hipStreamCreateWithFlags(&gr.xstream, hipStreamNonBlocking));
+        SD_HIP(hipEventCreateWithFlags(&gr.ev_bnd, hipEventDisableTiming));
+        SD_HIP(hipEventCreateWithFlags(&gr.ev_x, hipEventDisableTiming));
+        // halo planes are pulled straight from the neighbours' HBM (xGMI peer access)
+        for (int o : {gi - 1, gi + 1}) {
+            if (o < 0 || o >= G || dl[o] == gr.dev) continue;
+            int can = 0;
+            SD_HIP(hipDeviceCanAccessPeer(&can, gr.dev, dl[o]));
+            if (can) {
+                const hipError_t e = hipDeviceEnablePeerAccess(dl[o], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) SD_HIP(e);
+                (void)hipGetLastError();
+            }
+        }
+    }
+    stream_ = groups_[0].stream;
     if (p_.nranks > 1) {
+        DeviceGuard guard(p_.device);
         ncclUniqueId id;
         std::memcpy(&id, p_.comm_id, sizeof(id));
         SD_NCCL(ncclCommInitRank(&comm_, p_.nranks, id, p_.rank));
         p_.comm_id = nullptr;  // caller-owned; not retained
     }
-    slabs_.resize(p.local_slabs);
-    for (int s = 0; s < p.local_slabs; ++s) {
+    slabs_.resize(nslabs);
+    for (int s = 0; s < nslabs; ++s) {
         int64_t a, b;
-        slab_range(p.dims[2], p.local_slabs, s, &a, &b);
+        slab_range(p.dims[2], nslabs, s, &a, &b);
         SlabState& sl = slabs_[s];
+        sl.grp = s / p.local_slabs;
         sl.local_z0 = a;
         sl.g.nx = p.dims[0];
         sl.g.ny = p.dims[1];
@@ -63,54 +113,87 @@ Session::Session(const mvd_params& p) : p_(p) {
 }
 
 Session::~Session() {
-    DeviceGuard guard(p_.device);
-    if (stream_) (void)hipStreamSynchronize(stream_);
-    for (auto& r : trecs_) {
-        (void)hipEventDestroy(r.a);
-        (void)hipEventDestroy(r.b);
+    for (auto& gr : groups_) {
+        DeviceGuard guard(gr.dev);
+        if (gr.stream) (void)hipStreamSynchronize(gr.stream);
+        if (gr.xstream) (void)hipStreamSynchronize(gr.xstream);
     }
-    for (auto e : event_pool_) (void)hipEventDestroy(e);
-    slabs_.clear();
-    stats_dev_.release();
-    if (xstream_) (void)hipStreamSynchronize(xstream_);
-    if (comm_) ncclCommDestroy(comm_);
-    if (ev_bnd_) (void)hipEventDestroy(ev_bnd_);
-    if (ev_x_) (void)hipEventDestroy(ev_x_);
-    if (xstream_) (void)hipStreamDestroy(xstream_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+    {
+        DeviceGuard guard(p_.device);
+        for (auto& r : trecs_) {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        for (auto e : event_pool_) (void)hipEventDestroy(e);
+        if (comm_) ncclCommDestroy(comm_);
+    }
+    for (auto& sl : slabs_) {  // buffers and plans released on their own device
+        DeviceGuard guard(groups_[sl.grp].dev);
+        sl = SlabState{};
+    }
+    for (auto& gr : groups_) {
+        DeviceGuard guard(gr.dev);
+        gr.stats.release();
+        if (gr.ev_bnd) (void)hipEventDestroy(gr.ev_bnd);
+        if (gr.ev_x) (void)hipEventDestroy(gr.ev_x);
+        if (gr.xstream) (void)hipStreamDestroy(gr.xstream);
+        if (gr.stream) (void)hipStreamDestroy(gr.stream);
+    }
+}
+
+int Session::slab_device(int slab) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    return groups_[slabs_[slab].grp].dev;
+}
+
+void Session::sync_all() {
+    for (auto& gr : groups_) {
+        DeviceGuard guard(gr.dev);
+        SD_HIP(hipStreamSynchronize(gr.stream));
+        SD_HIP(hipStreamSynchronize(gr.xstream));
+    }
 }
 
 void Session::add_view(const float* img, const float* weight, const float* k1, const int* kdims,
                        bool device_ptrs) {
     SD_CHECK(img && weight && k1 && kdims, SPIMDECON_ERR_ARG, "null argument");
     SD_CHECK(!spectra_ready_, SPIMDECON_ERR_STATE, "views must be added before mvd_init");
-    DeviceGuard guard(p_.device);
     HostKernel hk;
     for (int d = 0; d < 3; ++d) {
         SD_CHECK(kdims[d] >= 1 && (kdims[d] & 1), SPIMDECON_ERR_ARG, "kernel dims must be odd");
         hk.dims[d] = kdims[d];
     }
     hk.data.assign(k1, k1 + int64_t(kdims[0]) * kdims[1] * kdims[2]);
-    k1_.push_back(std::move(hk));
-    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    // device pointers live on the first device; other groups copy them peer to peer
+    const hipMemcpyKind kind = device_ptrs ? hipMemcpyDefault : hipMemcpyHostToDevice;
     const int64_t plane = p_.dims[0] * p_.dims[1];
-    DBuf<float> tmp;
-    for (auto& sl : slabs_) {
-        const size_t esz = store_ == Store::F32 ? 4 : 2;
-        for (int which = 0; which < 2; ++which) {
-            const float* src = (which == 0 ? img : weight) + sl.local_z0 * plane;
-            DBuf<char> buf(size_t(sl.n) * esz);
-            if (store_ == Store::F32) {
-                SD_HIP(hipMemcpyAsync(buf.p, src, size_t(sl.n) * 4, kind, stream_));
-            } else {
-                if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
-                SD_HIP(hipMemcpyAsync(tmp.p, src, size_t(sl.n) * 4, kind, stream_));
-                launch_to_half(tmp.p, buf.p, sl.n, stream_);
+    std::vector<std::vector<DBuf<char>>> bufs(slabs_.size());
+    for (auto& gr : groups_) {
+        DeviceGuard guard(gr.dev);
+        DBuf<float> tmp;
+        for (int s = gr.s0; s < gr.s1; ++s) {
+            SlabState& sl = slabs_[s];
+            const size_t esz = store_ == Store::F32 ? 4 : 2;
+            for (int which = 0; which < 2; ++which) {
+                const float* src = (which == 0 ? img : weight) + sl.local_z0 * plane;
+                DBuf<char> buf(size_t(sl.n) * esz);
+                if (store_ == Store::F32) {
+                    SD_HIP(hipMemcpyAsync(buf.p, src, size_t(sl.n) * 4, kind, gr.stream));
+                } else {
+                    if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
+                    SD_HIP(hipMemcpyAsync(tmp.p, src, size_t(sl.n) * 4, kind, gr.stream));
+                    launch_to_half(tmp.p, buf.p, sl.n, gr.stream);
+                }
+                bufs[s].push_back(std::move(buf));
             }
-            (which == 0 ? sl.img : sl.w).push_back(std::move(buf));
         }
+        SD_HIP(hipStreamSynchronize(gr.stream));
     }
-    SD_HIP(hipStreamSynchronize(stream_));
+    for (size_t s = 0; s < slabs_.size(); ++s) {
+        slabs_[s].img.push_back(std::move(bufs[s][0]));
+        slabs_[s].w.push_back(std::move(bufs[s][1]));
+    }
+    k1_.push_back(std::move(hk));
     ++nviews_;
     kernels_ready_ = false;
 }
@@ -149,13 +232,14 @@ void Session::get_kernels(int view, float* k1, float* k2) const {
 }
 
 void Session::build_spectra() {
-    DeviceGuard guard(p_.device);
     int h[3] = {0, 0, 0};
     for (int v = 0; v < nviews_; ++v)
         for (int d = 0; d < 3; ++d) h[d] = std::max(h[d], k1_[v].dims[d] / 2);
     for (int d = 0; d < 3; ++d) halo_[d] = std::max(h[d], p_.halo[d]);
-    const int total_slabs = p_.local_slabs * p_.nranks;
+    const int total_slabs = int(slabs_.size()) * p_.nranks;
     for (auto& sl : slabs_) {
+        DeviceGuard guard(groups_[sl.grp].dev);
+        hipStream_t stream_ = groups_[sl.grp].stream;  // this slab's device stream
         SlabGeom& g = sl.g;
         g.cx = halo_[0];
         g.cy = halo_[1];
@@ -188,7 +272,7 @@ void Session::build_spectra() {
         SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
                               hipMemcpyHostToDevice, stream_));
         const float scale = float(1.0 / double(sl.pd.logical()));
-        DBuf<float> kd;
+        DBuf<float> kd;  // this slab's device
         if (backend_ == 1) {
             const size_t rf = size_t(sl.pd.real_floats());
             sl.Ra.alloc(rf);
@@ -246,16 +330,17 @@ void Session::build_spectra() {
                 }
             }
         }
+        SD_HIP(hipStreamSynchronize(stream_));
     }
-    SD_HIP(hipStreamSynchronize(stream_));
     spectra_ready_ = true;
 }
 
 double Session::init_psi(const float* psi_or_null) {
     SD_CHECK(nviews_ >= 1, SPIMDECON_ERR_STATE, "no views added");
-    DeviceGuard guard(p_.device);
     double avg = std::nan("");
     for (auto& sl : slabs_) {
+        DeviceGuard guard(groups_[sl.grp].dev);
+        hipStream_t st = groups_[sl.grp].stream;
         if (!sl.psi_a.p) {
             sl.psi_a.alloc(sl.n);
             sl.psi_b.alloc(sl.n);
@@ -267,26 +352,31 @@ double Session::init_psi(const float* psi_or_null) {
             for (int v = 0; v < nviews_; ++v) ptrs[v] = sl.img[v].p;
             sl.img_ptrs.alloc(nviews_);
             SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
-                                  hipMemcpyHostToDevice, stream_));
+                                  hipMemcpyHostToDevice, st));
+            SD_HIP(hipStreamSynchronize(st));
         }
     }
     if (psi_or_null) {
         const int64_t plane = p_.dims[0] * p_.dims[1];
         for (auto& sl : slabs_) {
+            DeviceGuard guard(groups_[sl.grp].dev);
+            hipStream_t st = groups_[sl.grp].stream;
             SD_HIP(hipMemcpyAsync(sl.psi, psi_or_null + sl.local_z0 * plane, size_t(sl.n) * 4,
-                                  hipMemcpyHostToDevice, stream_));
-            launch_clamp_min(sl.psi, sl.n, stream_);
+                                  hipMemcpyHostToDevice, st));
+            launch_clamp_min(sl.psi, sl.n, st);
         }
     } else {
         // FirstIteration + fuseFirstIteration (MVDeconvolution.java:192-235)
         double acc[2] = {0.0, 0.0};
         std::vector<double> part;
         for (auto& sl : slabs_) {
+            DeviceGuard guard(groups_[sl.grp].dev);
+            hipStream_t st = groups_[sl.grp].stream;
             DBuf<double> dpart(2 * 2048);
-            const int64_t nb = launch_first_iteration(sl.n, nviews_, store_, sl.img_ptrs.p, dpart.p, stream_);
+            const int64_t nb = launch_first_iteration(sl.n, nviews_, store_, sl.img_ptrs.p, dpart.p, st);
             part.resize(2 * nb);
-            SD_HIP(hipMemcpyAsync(part.data(), dpart.p, part.size() * 8, hipMemcpyDeviceToHost, stream_));
-            SD_HIP(hipStreamSynchronize(stream_));
+            SD_HIP(hipMemcpyAsync(part.data(), dpart.p, part.size() * 8, hipMemcpyDeviceToHost, st));
+            SD_HIP(hipStreamSynchronize(st));
             for (int64_t i = 0; i < nb; ++i) {
                 acc[0] += part[2 * i];
                 acc[1] += part[2 * i + 1];
@@ -295,9 +385,12 @@ double Session::init_psi(const float* psi_or_null) {
         allreduce_sum(acc, 2);
         avg = acc[0] / acc[1];  // NaN when no voxel has data
         const double a = std::isnan(avg) ? 0.5 : avg;  // :117-121
-        for (auto& sl : slabs_) launch_fill(sl.psi, sl.n, float(a), stream_);
+        for (auto& sl : slabs_) {
+            DeviceGuard guard(groups_[sl.grp].dev);
+            launch_fill(sl.psi, sl.n, float(a), groups_[sl.grp].stream);
+        }
     }
-    SD_HIP(hipStreamSynchronize(stream_));
+    sync_all();
     psi_ready_ = true;
     return avg;
 }
@@ -332,15 +425,14 @@ void Session::timing(double* out16) {
     for (int i = 0; i < 16; ++i) out16[i] = tacc_[i];
 }
 
-void Session::exchange(bool buffer_a, hipStream_t st) {
-    if (backend_ == 1) {
-        exchange_planes([](SlabState& sl, bool a) { return a ? sl.Ra.p : sl.Rb.p; }, buffer_a,
-                        size_t(slabs_[0].g.Sx * slabs_[0].g.My), st);
-    } else {
-        exchange_planes(
-            [](SlabState& sl, bool a) { return reinterpret_cast<float*>(a ? sl.C1.p : sl.C2.p); },
-            buffer_a, size_t(2 * slabs_[0].sp.Hp * slabs_[0].g.My), st);
-    }
+float* Session::buf_ptr(SlabState& sl, bool a, int backend) {
+    if (backend == 1) return a ? sl.Ra.p : sl.Rb.p;
+    return reinterpret_cast<float*>(a ? sl.C1.p : sl.C2.p);
+}
+
+size_t Session::plane_floats() const {
+    if (backend_ == 1) return size_t(slabs_[0].g.Sx * slabs_[0].g.My);
+    return size_t(2 * slabs_[0].sp.Hp * slabs_[0].g.My);
 }
 
 bool Session::split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest) const {
@@ -361,23 +453,26 @@ bool Session::split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest
     return true;
 }
 
-// halo exchange of cz padded z-planes between neighbouring slabs (local copies and RCCL)
-void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane, hipStream_t st) {
+// halo exchange of cz padded z-planes between neighbouring slabs of the only device
+// group (local copies) and with the neighbouring RCCL ranks
+void Session::exchange(bool which, hipStream_t st) {
     const int S = int(slabs_.size());
     if (S == 1 && p_.nranks == 1) return;
     const int cz = halo_[2];
     if (cz <= 0) return;
+    const size_t plane = plane_floats();
+    auto get = [&](SlabState& sl) { return buf_ptr(sl, which, backend_); };
     tstart(5, st);
     const size_t bytes = size_t(cz) * plane * sizeof(float);
     for (int s = 1; s < S; ++s) {
         SlabState& lo = slabs_[s - 1];
         SlabState& hi = slabs_[s];
         // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
-        SD_HIP(hipMemcpyAsync(get(lo, which) + size_t(lo.g.nz) * plane, get(hi, which), bytes,
+        SD_HIP(hipMemcpyAsync(get(lo) + size_t(lo.g.nz) * plane, get(hi), bytes,
                               hipMemcpyDeviceToDevice, st));
         // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
-        SD_HIP(hipMemcpyAsync(get(hi, which) + size_t(hi.g.Mz - cz) * plane,
-                              get(lo, which) + size_t(lo.g.nz - cz) * plane, bytes,
+        SD_HIP(hipMemcpyAsync(get(hi) + size_t(hi.g.Mz - cz) * plane,
+                              get(lo) + size_t(lo.g.nz - cz) * plane, bytes,
                               hipMemcpyDeviceToDevice, st));
     }
     if (p_.nranks > 1) {
@@ -385,15 +480,15 @@ void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_
         SD_NCCL(ncclGroupStart());
         if (p_.rank > 0) {
             SlabState& s0 = slabs_[0];
-            SD_NCCL(ncclSend(get(s0, which), count, ncclFloat, p_.rank - 1, comm_, st));
-            SD_NCCL(ncclRecv(get(s0, which) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
+            SD_NCCL(ncclSend(get(s0), count, ncclFloat, p_.rank - 1, comm_, st));
+            SD_NCCL(ncclRecv(get(s0) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
                              p_.rank - 1, comm_, st));
         }
         if (p_.rank < p_.nranks - 1) {
             SlabState& sl = slabs_[S - 1];
-            SD_NCCL(ncclSend(get(sl, which) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
+            SD_NCCL(ncclSend(get(sl) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
                              p_.rank + 1, comm_, st));
-            SD_NCCL(ncclRecv(get(sl, which) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
+            SD_NCCL(ncclRecv(get(sl) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
                              comm_, st));
         }
         SD_NCCL(ncclGroupEnd());
@@ -401,8 +496,56 @@ void Session::exchange_planes(float* (*get)(SlabState&, bool), bool which, size_
     tstop(st);
 }
 
+// Multi-device exchange, run by every group thread at the same point of the schedule.
+// (1) each group marks its boundary planes written (ev_bnd); barrier, so every event
+// is recorded before anyone waits on it; (2) each group's exchange stream waits for
+// its own and its neighbours' boundary events and PULLS the halo planes of its own
+// slabs (peer reads over xGMI; local copies between slabs of one device); barrier.
+// group_exchange_end: the compute stream waits for its own pulls and for the
+// neighbours' pulls out of its buffer (which its next x pass overwrites).
+void Session::group_exchange_begin(int gi, bool which, HostBarrier& bar) {
+    DevGroup& gr = groups_[gi];
+    const int G = int(groups_.size());
+    const int S = int(slabs_.size());
+    const int cz = halo_[2];
+    SD_HIP(hipEventRecord(gr.ev_bnd, gr.stream));
+    bar.wait();
+    for (int o : {gi - 1, gi, gi + 1})
+        if (o >= 0 && o < G) SD_HIP(hipStreamWaitEvent(gr.xstream, groups_[o].ev_bnd, 0));
+    if (gi == 0) tstart(5, gr.xstream);
+    if (cz > 0) {
+        const size_t plane = plane_floats();
+        const size_t bytes = size_t(cz) * plane * sizeof(float);
+        for (int s = gr.s0; s < gr.s1; ++s) {
+            SlabState& me = slabs_[s];
+            if (s > 0) {  // lower neighbour's last cz planes -> my lower halo [Mz - cz, Mz)
+                SlabState& lo = slabs_[s - 1];
+                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + size_t(me.g.Mz - cz) * plane,
+                                      buf_ptr(lo, which, backend_) + size_t(lo.g.nz - cz) * plane, bytes,
+                                      hipMemcpyDefault, gr.xstream));
+            }
+            if (s < S - 1) {  // upper neighbour's first cz planes -> my upper halo [nz, nz + cz)
+                SlabState& hi = slabs_[s + 1];
+                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + size_t(me.g.nz) * plane,
+                                      buf_ptr(hi, which, backend_), bytes, hipMemcpyDefault, gr.xstream));
+            }
+        }
+    }
+    if (gi == 0) tstop(gr.xstream);
+    SD_HIP(hipEventRecord(gr.ev_x, gr.xstream));
+    bar.wait();
+}
+
+void Session::group_exchange_end(int gi) {
+    DevGroup& gr = groups_[gi];
+    const int G = int(groups_.size());
+    for (int o : {gi - 1, gi, gi + 1})
+        if (o >= 0 && o < G) SD_HIP(hipStreamWaitEvent(gr.stream, groups_[o].ev_x, 0));
+}
+
 void Session::allreduce_sum(double* host, int n) {
     if (p_.nranks == 1) return;
+    DeviceGuard guard(p_.device);
     DBuf<double> d(n);
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
     SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclSum, comm_, stream_));
@@ -412,6 +555,7 @@ void Session::allreduce_sum(double* host, int n) {
 
 void Session::allreduce_max(double* host, int n) {
     if (p_.nranks == 1) return;
+    DeviceGuard guard(p_.device);
     DBuf<double> d(n);
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
     SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclMax, comm_, stream_));
@@ -423,16 +567,35 @@ void Session::run(int iters, double lambda, double* stats) {
     SD_CHECK(iters >= 0, SPIMDECON_ERR_ARG, "iters must be >= 0");
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "call mvd_init (or mvd_set_kernels) first");
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "call mvd_init_psi first");
-    DeviceGuard guard(p_.device);
     if (iters == 0) return;
     const int V = nviews_;
-    stats_dev_.alloc(size_t(iters) * V * 2);
-    if (backend_ == 1) run_rocfft(iters, lambda);
-    else run_engine(iters, lambda);
-    std::vector<double> st(size_t(iters) * V * 2);
-    SD_HIP(hipMemcpyAsync(st.data(), stats_dev_.p, st.size() * 8, hipMemcpyDeviceToHost, stream_));
-    SD_HIP(hipStreamSynchronize(stream_));
+    for (auto& gr : groups_) {
+        DeviceGuard guard(gr.dev);
+        gr.stats.alloc(size_t(iters) * V * 2);
+    }
+    if (backend_ == 1) {
+        DeviceGuard guard(p_.device);
+        run_rocfft(iters, lambda);
+    } else if (groups_.size() == 1) {
+        DeviceGuard guard(p_.device);
+        run_engine(0, iters, lambda, nullptr);
+    } else {
+        run_groups(iters, lambda);
+    }
+    // per-group {sum, max} -> totals (sum over groups in double, max)
+    std::vector<double> st(size_t(iters) * V * 2, 0.0), part(st.size());
+    for (size_t gi = 0; gi < groups_.size(); ++gi) {
+        DevGroup& gr = groups_[gi];
+        DeviceGuard guard(gr.dev);
+        SD_HIP(hipMemcpyAsync(part.data(), gr.stats.p, part.size() * 8, hipMemcpyDeviceToHost, gr.stream));
+        SD_HIP(hipStreamSynchronize(gr.stream));
+        for (size_t i = 0; i < st.size(); i += 2) {
+            st[i] = gi == 0 ? part[i] : st[i] + part[i];
+            st[i + 1] = gi == 0 ? part[i + 1] : std::max(st[i + 1], part[i + 1]);
+        }
+    }
     if (p_.nranks > 1) {
+        DeviceGuard guard(p_.device);
         std::vector<double> sums(size_t(iters) * V), maxs(size_t(iters) * V);
         for (size_t i = 0; i < sums.size(); ++i) {
             sums[i] = st[2 * i];
@@ -447,6 +610,7 @@ void Session::run(int iters, double lambda, double* stats) {
     }
     if (stats) std::copy(st.begin(), st.end(), stats);
     if (timing_on_) {
+        DeviceGuard guard(p_.device);
         for (auto& r : trecs_) {
             float ms = 0.f;
             SD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
@@ -457,6 +621,38 @@ void Session::run(int iters, double lambda, double* stats) {
         }
         trecs_.clear();
     }
+}
+
+// one host thread per device group; the exchanges keep them in step (HostBarrier)
+void Session::run_groups(int iters, double lambda) {
+    const int G = int(groups_.size());
+    HostBarrier bar(G);
+    std::vector<std::exception_ptr> errs(G);
+    std::vector<std::thread> th;
+    th.reserve(G);
+    for (int gi = 0; gi < G; ++gi) {
+        th.emplace_back([&, gi] {
+            try {
+                SD_HIP(hipSetDevice(groups_[gi].dev));
+                run_engine(gi, iters, lambda, &bar);
+            } catch (...) {
+                errs[gi] = std::current_exception();
+                bar.abort();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)  // the first failure that is not another group's abort
+        if (e) {
+            try {
+                std::rethrow_exception(e);
+            } catch (const Error& x) {
+                if (std::string(x.what()) != "device group aborted") throw;
+            }
+        }
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+    sync_all();
 }
 
 void Session::run_rocfft(int iters, double lambda) {
@@ -487,7 +683,7 @@ void Session::run_rocfft(int iters, double lambda) {
                                                      sl.psi_next, sl.Ra.p, sl.partials.p, !last, stream_);
                 tstop();
                 tstart(6);
-                launch_reduce_partials(sl.partials.p, nb, stats_dev_.p + (size_t(it) * V + v) * 2,
+                launch_reduce_partials(sl.partials.p, nb, groups_[0].stats.p + (size_t(it) * V + v) * 2,
                                        s > 0 ? 1 : 0, stream_);
                 tstop();
                 std::swap(sl.psi, sl.psi_next);
@@ -499,132 +695,146 @@ void Session::run_rocfft(int iters, double lambda) {
 
 // timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 fused z pass,
 // 4 initial psi x-pass, 5 halo exchange, 6 stats reduce, 7 banded y-z-y convolve
-void Session::run_engine(int iters, double lambda) {
+// (recorded by group 0 only)
+void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     const int V = nviews_;
+    DevGroup& gr = groups_[gi];
+    hipStream_t st = gr.stream;
+    const int s0 = gr.s0, s1 = gr.s1;
+    const bool tm = gi == 0;
+    auto T0 = [&](int cls) { if (tm) tstart(cls, st); };
+    auto T1 = [&]() { if (tm) tstop(st); };
     const int band = engine_band_tiles();
     const bool halo = slabs_.size() > 1 || p_.nranks > 1;
     // overlap: the x pass writes the planes the neighbours need first; their exchange
-    // (xstream_) runs while the x pass covers the rest of the slab
+    // (xstream) runs while the x pass covers the rest of the slab
     std::vector<PairRanges> bnd(slabs_.size()), rest(slabs_.size());
     bool overlap = halo;
-    for (size_t s = 0; s < slabs_.size(); ++s)
-        overlap = overlap && split_pairs(slabs_[s], bnd[s], rest[s]);
-    auto start_exchange = [&](bool buffer_a) {  // after the boundary launches on stream_
-        SD_HIP(hipEventRecord(ev_bnd_, stream_));
-        SD_HIP(hipStreamWaitEvent(xstream_, ev_bnd_, 0));
-        exchange(buffer_a, xstream_);
-        SD_HIP(hipEventRecord(ev_x_, xstream_));
+    for (int s = s0; s < s1; ++s) overlap = overlap && split_pairs(slabs_[s], bnd[s], rest[s]);
+    // exchange of one buffer: begin after the boundary launches, end before the y pass
+    auto xbegin = [&](bool buffer_a) {
+        if (bar) {
+            group_exchange_begin(gi, buffer_a, *bar);
+        } else {
+            SD_HIP(hipEventRecord(gr.ev_bnd, st));
+            SD_HIP(hipStreamWaitEvent(gr.xstream, gr.ev_bnd, 0));
+            exchange(buffer_a, gr.xstream);
+            SD_HIP(hipEventRecord(gr.ev_x, gr.xstream));
+        }
     };
-    auto finish_exchange = [&]() { SD_HIP(hipStreamWaitEvent(stream_, ev_x_, 0)); };
+    auto xend = [&]() {
+        if (bar) group_exchange_end(gi);
+        else SD_HIP(hipStreamWaitEvent(st, gr.ev_x, 0));
+    };
+    auto xfull = [&](bool buffer_a) {  // not overlapped
+        if (!halo) return;
+        if (bar) {
+            xbegin(buffer_a);
+            xend();
+        } else {
+            exchange(buffer_a, st);
+        }
+    };
+    auto convolve = [&](SlabState& sl, float2* Cb, const float2* K) {
+        if (band > 0) {
+            T0(7);
+            const bool banded = engine_convolve_banded(sl.sp, Cb, K, sl.kcompact, band, st);
+            T1();
+            if (banded) return;
+        }
+        T0(2); engine_ypass(sl.sp, Cb, false, st); T1();
+        T0(3);
+        if (sl.kcompact) engine_zpass_compact(sl.sp, Cb, K, st);
+        else engine_zpass(sl.sp, Cb, K, st);
+        T1();
+        T0(2); engine_ypass(sl.sp, Cb, true, st); T1();
+    };
 
-    for (auto& sl : slabs_) {
-        tstart(4);
-        engine_forward_psi(sl.sp, sl.psi, sl.C1.p, stream_);
-        tstop();
+    for (int s = s0; s < s1; ++s) {
+        T0(4);
+        engine_forward_psi(slabs_[s].sp, slabs_[s].psi, slabs_[s].C1.p, st);
+        T1();
     }
-    exchange(true, stream_);
+    xfull(true);
     for (int it = 0; it < iters; ++it) {
         for (int v = 0; v < V; ++v) {
             const bool last = (it == iters - 1) && (v == V - 1);
-            for (auto& sl : slabs_) {  // convolve1
-                if (band > 0) {
-                    tstart(7);
-                    const bool banded = engine_convolve_banded(sl.sp, sl.C1.p, sl.e1spec[v].p, sl.kcompact, band, stream_);
-                    tstop();
-                    if (banded) continue;
-                }
-                tstart(2); engine_ypass(sl.sp, sl.C1.p, false, stream_); tstop();
-                tstart(3);
-                if (sl.kcompact) engine_zpass_compact(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_);
-                else engine_zpass(sl.sp, sl.C1.p, sl.e1spec[v].p, stream_);
-                tstop();
-                tstart(2); engine_ypass(sl.sp, sl.C1.p, true, stream_); tstop();
-            }
+            for (int s = s0; s < s1; ++s) convolve(slabs_[s], slabs_[s].C1.p, slabs_[s].e1spec[v].p);
             // quotient (+ forward x of the quotient) and its halo exchange
             if (overlap) {
-                for (size_t s = 0; s < slabs_.size(); ++s) {
+                for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, bnd[s], stream_); tstop();
+                    T0(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, bnd[s], st); T1();
                 }
-                start_exchange(false);
-                for (size_t s = 0; s < slabs_.size(); ++s) {
+                xbegin(false);
+                for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    tstart(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, rest[s], stream_); tstop();
+                    T0(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, rest[s], st); T1();
                 }
-                finish_exchange();
+                xend();
             } else {
-                for (auto& sl : slabs_) {
-                    tstart(1);
-                    engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, all_pairs(sl.sp), stream_);
-                    tstop();
+                for (int s = s0; s < s1; ++s) {
+                    SlabState& sl = slabs_[s];
+                    T0(1);
+                    engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, all_pairs(sl.sp), st);
+                    T1();
                 }
-                exchange(false, stream_);
+                xfull(false);
             }
-            for (auto& sl : slabs_) {  // convolve2
-                if (band > 0) {
-                    tstart(7);
-                    const bool banded = engine_convolve_banded(sl.sp, sl.C2.p, sl.e2spec[v].p, sl.kcompact, band, stream_);
-                    tstop();
-                    if (banded) continue;
-                }
-                tstart(2); engine_ypass(sl.sp, sl.C2.p, false, stream_); tstop();
-                tstart(3);
-                if (sl.kcompact) engine_zpass_compact(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_);
-                else engine_zpass(sl.sp, sl.C2.p, sl.e2spec[v].p, stream_);
-                tstop();
-                tstart(2); engine_ypass(sl.sp, sl.C2.p, true, stream_); tstop();
-            }
+            for (int s = s0; s < s1; ++s) convolve(slabs_[s], slabs_[s].C2.p, slabs_[s].e2spec[v].p);
             // update (+ forward x of the next psi) and its halo exchange
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
-            for (size_t s = 0; s < slabs_.size(); ++s) {
+            for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
-                tstart(0);
+                T0(0);
                 nb[s] = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
-                                      last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp),
-                                      stream_);
-                tstop();
+                                      last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp), st);
+                T1();
             }
             if (ov) {
-                start_exchange(true);
-                for (size_t s = 0; s < slabs_.size(); ++s) {
+                xbegin(true);
+                for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    tstart(0);
+                    T0(0);
                     nb[s] += engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
-                                           sl.C1.p, sl.partials.p + 2 * nb[s], rest[s], stream_);
-                    tstop();
+                                           sl.C1.p, sl.partials.p + 2 * nb[s], rest[s], st);
+                    T1();
                 }
             }
-            for (size_t s = 0; s < slabs_.size(); ++s) {
+            for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
-                tstart(6);
-                launch_reduce_partials(sl.partials.p, nb[s], stats_dev_.p + (size_t(it) * V + v) * 2,
-                                       s > 0 ? 1 : 0, stream_);
-                tstop();
+                T0(6);
+                launch_reduce_partials(sl.partials.p, nb[s], gr.stats.p + (size_t(it) * V + v) * 2,
+                                       s > s0 ? 1 : 0, st);
+                T1();
                 std::swap(sl.psi, sl.psi_next);
             }
-            if (ov) finish_exchange();
-            else if (!last) exchange(true, stream_);
+            if (ov) xend();
+            else if (!last) xfull(true);
         }
     }
 }
 
 void Session::apply_mask() {
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
-    DeviceGuard guard(p_.device);
-    for (auto& sl : slabs_) launch_mask(sl.psi, sl.n, nviews_, store_, sl.img_ptrs.p, stream_);
-    SD_HIP(hipStreamSynchronize(stream_));
+    for (auto& sl : slabs_) {
+        DeviceGuard guard(groups_[sl.grp].dev);
+        launch_mask(sl.psi, sl.n, nviews_, store_, sl.img_ptrs.p, groups_[sl.grp].stream);
+    }
+    sync_all();
 }
 
 void Session::get_psi(float* out) {
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
     SD_CHECK(out, SPIMDECON_ERR_ARG, "null output");
-    DeviceGuard guard(p_.device);
     const int64_t plane = p_.dims[0] * p_.dims[1];
-    for (auto& sl : slabs_)
+    for (auto& sl : slabs_) {
+        DeviceGuard guard(groups_[sl.grp].dev);
         SD_HIP(hipMemcpyAsync(out + sl.local_z0 * plane, sl.psi, size_t(sl.n) * 4,
-                              hipMemcpyDeviceToHost, stream_));
-    SD_HIP(hipStreamSynchronize(stream_));
+                              hipMemcpyDeviceToHost, groups_[sl.grp].stream));
+    }
+    sync_all();
 }
 
 float* Session::psi_device(int slab) {
@@ -643,6 +853,13 @@ int Session::zpass_mode(int slab) const {
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
     if (backend_ != 0) return -1;
     return engine_zpass_mode(slabs_[slab].sp, slabs_[slab].kcompact);
+}
+
+int Session::xpass_mode(int slab) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
+    if (backend_ != 0) return -2;
+    return slabs_[slab].sp.xmode_update;
 }
 
 int Session::kernel_planes(int slab) const {

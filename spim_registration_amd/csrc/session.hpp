@@ -9,13 +9,23 @@
 //   Rb = pad_one(img_v > 0 ? img_v / Ra : 1)                    computeQuotient
 //   Rb = C2R(R2C(Rb) * FFT(K2_v))    convolve2
 //   psi' = update(psi, Rb, w_v);  Ra = pad_mirror(psi')         computeFinalValues
-// The volume is split into z-slabs (local virtual slabs and/or one slab per
-// RCCL rank); halos of c_z padded planes are exchanged after each pad.
+// The volume is split into z-slabs (local virtual slabs, slabs on several
+// devices of this process, and/or one slab range per RCCL rank); halos of c_z
+// padded planes are exchanged after each pad.
+//
+// Several devices in one process (mvd_create_devices, the reference's
+// MVDeconFFT(..., int[] deviceList, ...) driven from one JVM, MVDeconFFT.java:58-64,
+// 424-446): each device group owns consecutive slabs, a stream and an exchange
+// stream; mvd_run drives every group from its own host thread, and the halo planes
+// are pulled from the neighbouring groups' HBM (peer copies over xGMI) between two
+// host barriers per exchange (events recorded before any stream waits on them).
 #pragma once
 
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -27,6 +37,7 @@
 namespace spimdecon {
 
 struct SlabState {
+    int grp = 0;           // device group (index into Session::groups_)
     SlabGeom g{};
     PadDims pd;
     int64_t local_z0 = 0;  // first plane within this rank's z-range
@@ -52,9 +63,37 @@ struct TimingRec {
     hipEvent_t a, b;
 };
 
+// one device of a multi-device session (or the only one)
+struct DevGroup {
+    int dev = 0;
+    int s0 = 0, s1 = 0;                    // slabs [s0, s1)
+    hipStream_t stream = nullptr;
+    hipStream_t xstream = nullptr;          // halo exchanges overlapped with the interior x pass
+    hipEvent_t ev_bnd = nullptr, ev_x = nullptr;
+    DBuf<double> stats;                     // iters * V * {sum, max} of this group's slabs
+};
+
+// reusable host barrier for the group threads; abort() releases every waiter with an
+// error so that one failing thread cannot deadlock the others
+class HostBarrier {
+public:
+    explicit HostBarrier(int n) : n_(n) {}
+    void wait();
+    void abort();
+
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int n_, count_ = 0;
+    uint64_t gen_ = 0;
+    bool aborted_ = false;
+};
+
 class Session {
 public:
-    explicit Session(const mvd_params& p);
+    // devs: the device of each group (repeats allowed: groups sharing one GPU run the
+    // multi-device code path on it); empty = {p.device}
+    explicit Session(const mvd_params& p, const std::vector<int>& devs = {});
     ~Session();
 
     void add_view(const float* img, const float* weight, const float* k1, const int* kdims,
@@ -70,18 +109,30 @@ public:
     void fft_dims(int slab, int64_t* out3) const;
     int kernel_planes(int slab) const;
     int zpass_mode(int slab) const;
-    hipStream_t stream() const { return stream_; }
+    int xpass_mode(int slab) const;
+    hipStream_t stream() const { return groups_[0].stream; }
+    int ndevices() const { return int(groups_.size()); }
+    int slab_device(int slab) const;
     void enable_timing(bool on) { timing_on_ = on; }
     void timing(double* out16);
 
 private:
     void build_spectra();
+    static float* buf_ptr(SlabState& sl, bool a, int backend);
+    size_t plane_floats() const;
+    // halo exchange of one buffer (C1/Ra when buffer_a) among the slabs of group gi and,
+    // with one group, over RCCL; issued on st (single group)
     void exchange(bool buffer_a, hipStream_t st);
-    void exchange_planes(float* (*get)(SlabState&, bool), bool which, size_t plane_floats, hipStream_t st);
+    // multi-group exchange protocol (called by every group thread in step)
+    void group_exchange_begin(int gi, bool buffer_a, HostBarrier& bar);
+    void group_exchange_end(int gi);
     // x-pass pair ranges of a slab: the planes its neighbours need (bnd) and the rest
     bool split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest) const;
     void run_rocfft(int iters, double lambda);
-    void run_engine(int iters, double lambda);
+    // the engine schedule of group gi; bar == nullptr: the only group (RCCL halos)
+    void run_engine(int gi, int iters, double lambda, HostBarrier* bar);
+    void run_groups(int iters, double lambda);
+    void sync_all();
     void allreduce_sum(double* host, int n);
     void allreduce_max(double* host, int n);
     void tstart(int cls, hipStream_t st = nullptr);
@@ -90,9 +141,8 @@ private:
     mvd_params p_{};
     int backend_ = 0;  // 0 = fused spectral engine, 1 = rocFFT (mvd_params.fft_backend)
     Store store_ = Store::F32;
-    hipStream_t stream_ = nullptr;
-    hipStream_t xstream_ = nullptr;  // halo exchanges overlapped with the interior x pass
-    hipEvent_t ev_bnd_ = nullptr, ev_x_ = nullptr;
+    std::vector<DevGroup> groups_;
+    hipStream_t stream_ = nullptr;   // groups_[0].stream
     ncclComm_t comm_ = nullptr;
     std::vector<SlabState> slabs_;
     std::vector<HostKernel> k1_, k2_;
@@ -101,7 +151,6 @@ private:
     bool kernels_ready_ = false;
     bool spectra_ready_ = false;
     bool psi_ready_ = false;
-    DBuf<double> stats_dev_;
     bool timing_on_ = false;
     std::vector<TimingRec> trecs_;
     int tcur_ = -1;

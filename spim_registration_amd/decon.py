@@ -140,7 +140,10 @@ class Session:
 
     def __init__(self, dims_xyz, device=0, local_slabs=1, nranks=1, rank=0, comm_id=None,
                  nz_global=None, z_offset=0, storage_fp16=False, ij_threads=8, halo=None,
-                 fft_backend="engine", fft_pad_policy="auto"):
+                 fft_backend="engine", fft_pad_policy="auto", devices=None):
+        """``devices``: several GPUs of this process (``mvd_create_devices``; the
+        reference's ``deviceList``, MVDeconFFT.java:58-64) -- the volume is split into
+        len(devices) * local_slabs z-slabs and one ``run`` drives all of them."""
         self.lib = _lib.load()
         p = _lib.MvdParams()
         self.lib.mvd_params_default(C.byref(p))
@@ -162,7 +165,13 @@ class Session:
             for d in range(3):
                 p.halo[d] = int(halo[d])
         h = C.c_void_p()
-        check(self.lib.mvd_create(C.byref(p), C.byref(h)))
+        if devices is not None and len(devices) > 1:
+            devs = np.ascontiguousarray(devices, np.int32)
+            check(self.lib.mvd_create_devices(_lib.iptr(devs), len(devs), C.byref(p), C.byref(h)))
+        else:
+            if devices:
+                p.device = int(devices[0])
+            check(self.lib.mvd_create(C.byref(p), C.byref(h)))
         self.h = h
         self.params = p
         self.nviews = 0
@@ -251,6 +260,22 @@ class Session:
         check(self.lib.mvd_zpass_mode(self.h, int(slab), C.byref(out)))
         return out.value
 
+    def xpass_mode(self, slab=0):
+        """x pass of the last update launch: 2 two-factor tiles, 1 per-wave rows, 0 Stockham."""
+        out = C.c_int()
+        check(self.lib.mvd_xpass_mode(self.h, int(slab), C.byref(out)))
+        return out.value
+
+    def num_devices(self):
+        out = C.c_int()
+        check(self.lib.mvd_num_devices(self.h, C.byref(out)))
+        return out.value
+
+    def slab_device(self, slab):
+        out = C.c_int()
+        check(self.lib.mvd_slab_device(self.h, int(slab), C.byref(out)))
+        return out.value
+
     def enable_timing(self, on=True):
         check(self.lib.mvd_enable_timing(self.h, int(on)))
 
@@ -283,8 +308,10 @@ class MVDeconvolution:
         if not data:
             raise ValueError("no views")
         shape = data[0].get_image().shape
-        dev = data[0].device_list[0]
-        self.session = Session((shape[2], shape[1], shape[0]), device=dev, local_slabs=local_slabs,
+        # MVDeconFFT.java:91-100: every view carries the same device list; all of its GPUs
+        # share the volume (z-slabs, halo exchange inside the library)
+        devs = list(data[0].device_list)
+        self.session = Session((shape[2], shape[1], shape[0]), devices=devs, local_slabs=local_slabs,
                                storage_fp16=storage_fp16, ij_threads=ij_threads)
         for v in data:
             self.session.add_view(v.get_image(), v.get_weight(), v.kernel1)

@@ -1,0 +1,131 @@
+"""GPU: one session over several devices of this process (``mvd_create_devices``)
+and the virtual-slab paths of the fast x tiles.
+
+The reference drives several GPUs from one JVM through
+``MVDeconFFT(..., int[] deviceList, ...)`` (MVDeconFFT.java:58-64,91-100,424-446).
+Here one ``mvd_run`` drives every device of the list from its own host thread;
+the halo planes move between neighbouring devices as peer copies.  Device ids
+may repeat, so the one-GPU box runs exactly the multi-device code (threads,
+barriers, cross-stream events, pull copies) with every group on device 0.
+
+Tolerances: psi within 1e-5 relative L2 of the single-slab session (only the
+FFT rounding of the slab-sized transforms differs) and 1e-4 of the oracle (the
+north-star bound); per-view stats within rtol 1e-4 of the single-slab session.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+from oracle import mvdecon_ref as ref
+from spim_registration_amd import synthetic
+from spim_registration_amd._lib import SpimDeconError
+from spim_registration_amd.decon import MVDeconFFT, MVDeconInput, MVDeconvolution, PSFTYPE, Session
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+# nx % 4 == 0 and Mx = 256 = 16 * 16 (two-factor x table): the update / quotient
+# passes run the row-pair tiles (k_xtile), with slab row maps and the split
+# boundary / rest launches of the overlapped exchange
+TILE_SHAPE = (60, 20, 248)      # [z, y, x]
+TILE_K = (9, 7, 9)              # kx, ky, kz -> cz = 4
+
+
+def tile_case(V=2, cid=11, partial=True):
+    return synthetic.make_views(TILE_SHAPE, V, config_id=cid, ksize=TILE_K, weights="blend",
+                                partial=partial, bead_density=1.0 / 6 ** 3)
+
+
+def run_session(imgs, ws, ks, iters=3, lam=0.006, psftype=PSFTYPE.OPTIMIZATION_I, **kw):
+    shape = imgs[0].shape
+    with Session(shape[::-1], **kw) as s:
+        for i, w, k in zip(imgs, ws, ks):
+            s.add_view(i, w, k)
+        s.init(psftype)
+        s.init_psi()
+        st = s.run(iters, lam)
+        s.apply_mask()
+        nslab = kw.get("local_slabs", 1) * max(1, len(kw.get("devices") or [0]))
+        modes = [s.xpass_mode(i) for i in range(nslab)]
+        ndev = s.num_devices()
+        devs = [s.slab_device(i) for i in range(nslab)]
+        return s.get_psi(), st, modes, ndev, devs
+
+
+@pytest.fixture(scope="module")
+def tile_ref():
+    imgs, ws, ks, _ = tile_case()
+    psi, st, modes, _, _ = run_session(imgs, ws, ks)
+    assert modes == [2], modes          # the two-factor x tiles ran
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
+    assert rel_l2(psi, res.psi) < TOL
+    return imgs, ws, ks, psi, st, res
+
+
+@pytest.mark.parametrize("slabs", [2, 3, 6])
+def test_virtual_slabs_on_tile_path(gpu, tile_ref, slabs):
+    """local slabs with the k_xtile passes (overlapped boundary / rest
+    split, psi x tiles on slab row maps, two-launch stats partials)."""
+    imgs, ws, ks, psi1, st1, res = tile_ref
+    psi, st, modes, ndev, _ = run_session(imgs, ws, ks, local_slabs=slabs)
+    assert ndev == 1 and modes == [2] * slabs, modes
+    assert rel_l2(psi, psi1) < 1e-5
+    np.testing.assert_allclose(st, st1, rtol=1e-4)
+    assert rel_l2(psi, res.psi) < TOL
+
+
+@pytest.mark.parametrize("devices,slabs", [([0, 0], 1), ([0, 0, 0], 1), ([0, 0], 2), ([0, 0, 0, 0], 3)])
+def test_device_groups_match_single(gpu, tile_ref, devices, slabs):
+    """Several device groups in one session: one host thread per group, halo pulls
+    between groups, stats combined over the groups."""
+    imgs, ws, ks, psi1, st1, res = tile_ref
+    psi, st, modes, ndev, devs = run_session(imgs, ws, ks, devices=devices, local_slabs=slabs)
+    assert ndev == len(devices)
+    assert devs == [d for d in devices for _ in range(slabs)]
+    assert modes == [2] * (len(devices) * slabs), modes
+    assert rel_l2(psi, psi1) < 1e-5
+    np.testing.assert_allclose(st, st1, rtol=1e-4)
+    assert rel_l2(psi, res.psi) < TOL
+
+
+def test_mvdeconvolution_device_list(gpu):
+    """decon.MVDeconvolution routes the views' device_list into one multi-device
+    session (the reference's deviceList), not just its first entry."""
+    imgs, ws, ks, _ = synthetic.make_views((40, 20, 22), 3, config_id=5, ksize=(5, 7, 9),
+                                           weights="blend", partial=True, bead_density=1.0 / 6 ** 3)
+    inp = MVDeconInput()
+    for i, w, k in zip(imgs, ws, ks):
+        inp.add(MVDeconFFT(i, w, k, device_list=[0, 0, 0]))
+    dec = MVDeconvolution(inp, PSFTYPE.EFFICIENT_BAYESIAN, 4, 0.006)
+    assert dec.session.num_devices() == 3
+    psi = dec.get_psi()
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.EFFICIENT_BAYESIAN, 4, 0.006)
+    assert rel_l2(psi, res.psi) < TOL
+    np.testing.assert_allclose(dec.stats[:, :, 0], np.array(res.stats)[:, :, 0], rtol=1e-3)
+    assert ((psi == 0) == (res.psi == 0)).all()
+
+
+def test_device_groups_fp16_and_initial_image(gpu):
+    imgs, ws, ks, _ = tile_case(V=3, cid=12, partial=False)
+    init = imgs[1].copy()
+    out = []
+    for kw in ({}, {"devices": [0, 0]}):
+        with Session(TILE_SHAPE[::-1], storage_fp16=True, **kw) as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.INDEPENDENT)
+            s.init_psi(init)
+            s.run(2, 0.0)
+            s.run(1, 0.0)       # continues from the resident psi on every device
+            out.append(s.get_psi())
+    assert rel_l2(out[1], out[0]) < 1e-5
+
+
+def test_device_groups_reject_bad_arguments(gpu):
+    with pytest.raises(SpimDeconError):
+        Session((16, 16, 16), devices=[0, 0], fft_backend="rocfft")
+    with pytest.raises(SpimDeconError):
+        Session((16, 16, 3), devices=[0, 0], local_slabs=2)     # 4 slabs > 3 planes
+    with pytest.raises(SpimDeconError):
+        Session((16, 16, 16), devices=[0, -1])
