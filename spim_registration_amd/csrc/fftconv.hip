@@ -536,7 +536,7 @@ XArgs base_args(const SpectralPlan& p) {
 }
 
 // two-factor x tiles: lengths >= 256 of the fast-path table
-#define SD_X2F_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24) M(20, 32) M(25, 32) M(30, 35)
+#define SD_X2F_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24) M(20, 32) M(25, 32) M(30, 35) M(42, 50)
 
 bool aligned_to(const void* q, size_t n) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % n == 0; }
 
@@ -597,7 +597,7 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     }
 #define SD_XT_N(A, B, NP) \
     SD_XT(0, A, B, false, NP) SD_XT(1, A, B, false, NP) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true, NP) SD_XT(1, A, B, true, NP) }
-#define SD_XT_S(A, B) SD_XT_N(A, B, 16) SD_XT_N(A, B, 8)
+#define SD_XT_S(A, B) if constexpr ((A) * (B) <= 1204) { SD_XT_N(A, B, 16) } SD_XT_N(A, B, 8)
     SD_X2F_SIZES(SD_XT_S)
 #undef SD_XT_S
 #undef SD_XT_N
@@ -698,8 +698,11 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // nout: z planes the pass must produce (AXIS 1: planes transformed; AXIS 2 fused
     // modes: planes stored) -- the RL loop only reads the nz interior planes back
     if (nout < 0) nout = int(p.g.Mz);
-    const int TX = k2fTX;  // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
     const int L = f.L;
+    // 16-column tiles (128-B row segments); 8 columns when a 16-column tile of the
+    // length would not fit the LDS (L > 1204, e.g. 2100 for 2048-wide volumes).
+    // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
+    const int TX = size_t(L * k2fTX + L) * sizeof(float2) <= 160 * 1024 ? k2fTX : 8;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
     const size_t lds = size_t(L * TX + L + (MODE == 5 ? f.n2 * TX : 0)) * sizeof(float2);
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
@@ -709,8 +712,10 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // the fused z modes hold two length-N2 vectors per thread: TR = 64 (N2 > 32) would
     // spill, so long lengths run them on the Stockham column pass
     if (MODE >= 2 && tr == 64) return false;
-    if (lds > (tr == 64 ? 160 : 80) * 1024 || bytes >= (uint64_t(1) << 31)) return false;
+    if (lds > (tr == 64 ? 160 : 80) * 1024 || (AXIS == 2 && bytes >= (uint64_t(1) << 31))) return false;
     if (MODE == 5 && (AXIS != 2 || kplanes > f.n2)) return false;
+    // AXIS 1 resources span one z plane from the tile's first column
+    const uint32_t rbytes = AXIS == 1 ? uint32_t(uint64_t(p.g.My * p.Hp) * sizeof(float2)) : uint32_t(bytes);
     if (ntxb < 0) ntxb = int(p.Hp / TX);
     SD_CHECK(tx0 >= 0 && ntxb > 0 && tx0 + ntxb <= p.Hp / TX, SPIMDECON_ERR_ARG, "bad column band");
     const int64_t ntiles = int64_t(ntxb) * (AXIS == 1 ? nout : p.g.My);
@@ -725,13 +730,13 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
             SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv>), \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
             hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv>), dim3(grid), dim3(T * TRv), lds, s,     \
-                               p.g, p.Hp, f.tw, C, K, uint32_t(bytes), tx0, ntxb, kc, uint32_t(kbytes), \
+                               p.g, p.Hp, f.tw, C, K, rbytes, tx0, ntxb, kc, uint32_t(kbytes),         \
                                nout);                                                              \
             done = true;                                                                                   \
         }                                                                                                  \
     }
 #define SD_2F_C(A, B) \
-    SD_2F_C1(A, B, 16)
+    SD_2F_C1(A, B, 16) if constexpr ((A) * (B) > 1204) { SD_2F_C1(A, B, 8) }
     SD_2F_SIZES(SD_2F_C)
 #undef SD_2F_C
 #undef SD_2F_C1
@@ -944,7 +949,7 @@ bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
     // Mz >= KC: the wrap copies of k_zdirect fill every window slot only then (a
     // window slot left unwritten would multiply stale LDS by a zero tap: 0 * NaN)
     return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC && lds <= 160 * 1024 &&
-           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) < (uint64_t(1) << 31);
+           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
 }
 
 bool engine_zdirect_ok(const SpectralPlan& p) {
@@ -963,8 +968,9 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         const int64_t ntiles = (p.Hp / kZdTX) * p.g.My;
         const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
         const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
-        const uint32_t bytes = uint32_t(uint64_t(p.spectrum_elems()) * sizeof(float2));
-        const uint32_t kbytes = uint32_t(uint64_t(engine_kernel_compact_elems(p)) * sizeof(float2));
+        // per-tile ranges (k_zdirect rebuilds its resources at each tile's first column)
+        const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
+        const uint32_t kbytes = uint32_t(uint64_t(p.g.My * p.Hp) * (2 * p.g.cz + 1) * sizeof(float2));
         const float kscale = float(p.g.Mz);
         bool done = false;
 #define SD_ZD(KCV)                                                                                   \
