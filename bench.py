@@ -55,7 +55,18 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--backend", default="engine", choices=["engine", "rocfft"])
     ap.add_argument("--pad-policy", default="auto", choices=["auto", "fast", "smooth"])
-    return ap.parse_args()
+    ap.add_argument("--local-slabs", type=int, default=1, help="z-slabs per process (virtual shards)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the global volume --shape (default 1024 1024 512, EFFICIENT_BAYESIAN "
+                         "lambda 0.006 = BASELINE configs[2]) is split into N z-slabs, one per rank")
+    ap.add_argument("--no-default-mode", action="store_true",
+                    help="skip the second measurement in the reference default mode (OPTIMIZATION_I, 0.006)")
+    a = ap.parse_args()
+    if a.strong and a.shape is None:
+        a.shape = [1024, 1024, 512]
+        if a.psftype == "INDEPENDENT" and a.lam == 0.0:
+            a.psftype, a.lam = "EFFICIENT_BAYESIAN", 0.006
+    return a
 
 
 # engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
@@ -89,29 +100,45 @@ def pmc_traffic(cls, M, args):
             f"{d['file']}: " + " / ".join(n for n, _ in hits) + (" (mean)" if len(hits) > 1 else ""))
 
 
-def cpu_baseline(args):
-    """The oracle (numpy + scipy.fft float32, multithreaded) on a bounded sample:
-    V views of cpu_size^3 with the same PSFs; 1 warm-up + 2 timed iterations."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, shape_xyz):
+    """The oracle (numpy + scipy.fft float32, multithreaded) on the SAME workload as
+    the GPU line (V views of the benchmarked volume, same PSFs): one RL iteration,
+    timed from an initialised psi.  Threads: the box's CPU share (OMP_NUM_THREADS,
+    16 per GPU on the MI355X pool; os.cpu_count() elsewhere) -- reported as `cores`
+    next to the host's logical CPU count and model."""
     from oracle import mvdecon_ref as ref
     from spim_registration_amd import synthetic
 
-    n = args.cpu_size
-    cores = min(os.cpu_count() or 1, 16)
-    imgs, ws, psfs, _ = synthetic.make_views((n, n, n), args.views, config_id=1,
+    nx, ny, nz = shape_xyz
+    if args.cpu_size != 256:          # explicit smaller sample (cube of --cpu-size)
+        nx = ny = nz = args.cpu_size
+    host_cpus = os.cpu_count() or 1
+    cores = int(os.environ.get("OMP_NUM_THREADS", host_cpus))
+    imgs, ws, psfs, _ = synthetic.make_views((nz, ny, nx), args.views, config_id=1,
                                              ksize=(args.ksize,) * 3, weights="blend")
     k1s, k2s = ref.prepare_kernels(psfs, ref.PSFTYPE[args.psftype], 8)
     _, avg = ref.first_iteration(imgs)
     psi = np.full(imgs[0].shape, np.float32(avg), np.float32)
-    psi, _ = ref.run_iteration(psi, imgs, ws, k1s, k2s, args.lam, "f32", cores)
     t0 = time.perf_counter()
-    iters = 2
-    for _ in range(iters):
-        psi, _ = ref.run_iteration(psi, imgs, ws, k1s, k2s, args.lam, "f32", cores)
-    dt = (time.perf_counter() - t0) / iters
-    return {"value": round(n ** 3 / dt / 1e6, 3), "unit": "Mvoxels/s per RL iteration",
-            "cores": cores, "kind": "port",
-            "sample": f"{args.views}-view {n}^3, {args.ksize}^3 PSF, {args.psftype}, 2 timed iterations "
-                      f"(numpy + scipy.fft float32, workers={cores}); stand-in for the Java/ImgLib2 CPU path"}
+    psi, _ = ref.run_iteration(psi, imgs, ws, k1s, k2s, args.lam, "f32", cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(nx * ny * nz / dt / 1e6, 3), "unit": "Mvoxels/s per RL iteration",
+            "cores": cores, "host_cpus": host_cpus, "cpu_model": cpu_model(), "kind": "port",
+            "seconds": round(dt, 2),
+            "sample": f"{args.views}-view {nx}x{ny}x{nz} (the benchmarked volume), {args.ksize}^3 PSF, "
+                      f"{args.psftype} lambda={args.lam}, 1 timed iteration (numpy + scipy.fft float32, "
+                      f"workers={cores}); stand-in for the Java/ImgLib2 CPU path"}
 
 
 def main():
@@ -129,43 +156,70 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
-    comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
 
     nx, ny, nz = args.shape if args.shape else (args.size,) * 3
     V = args.views
-    nz_g = nz * world
+    if args.strong:      # the global volume is fixed; rank r owns z-slab r of N
+        from spim_registration_amd.distributed import slab_range
+        nz_g = nz
+        z0, z1 = slab_range(nz_g, world, rank)
+        nz = z1 - z0
+    else:                # weak scaling: every rank adds an nz-plane slab
+        nz_g = nz * world
+        z0 = rank * nz
     imgs, ws, psfs = synthetic.make_views_torch((nz, ny, nx), V, config_id=1 + rank,
                                                 ksize=(args.ksize,) * 3, device=f"cuda:{local}")
     torch.cuda.synchronize()
-    sess = Session((nx, ny, nz), device=local, nranks=world, rank=rank, comm_id=comm_id,
-                   nz_global=nz_g, z_offset=rank * nz, storage_fp16=args.fp16,
-                   fft_backend=args.backend, fft_pad_policy=args.pad_policy)
-    for i, w, k in zip(imgs, ws, psfs):
-        sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
-    del imgs, ws
-    torch.cuda.empty_cache()
-    sess.init(PSFTYPE[args.psftype])
-    sess.init_psi()
-    M = sess.fft_dims(0)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    # warm-up (rocFFT kernels, caches)
-    if args.warmup:
-        sess.run(args.warmup, args.lam)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sess.run(args.steps, args.lam)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    barrier()
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+    def make_session(psftype):
+        # a fresh RCCL id per communicator (an id bootstraps one communicator only)
+        comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
+        s = Session((nx, ny, nz), device=local, nranks=world, rank=rank, comm_id=comm_id,
+                    nz_global=nz_g, z_offset=z0, storage_fp16=args.fp16, local_slabs=args.local_slabs,
+                    fft_backend=args.backend, fft_pad_policy=args.pad_policy)
+        for i, w, k in zip(imgs, ws, psfs):
+            s.add_view_device(i.data_ptr(), w.data_ptr(), k)
+        s.init(PSFTYPE[psftype])
+        s.init_psi()
+        return s
+
+    def timed(s, lam):
+        """W warm-up iterations (untimed), then K iterations between barriers and
+        device syncs; the max over ranks."""
+        if args.warmup:
+            s.run(args.warmup, lam)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.run(args.steps, lam)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        barrier()
+        if world > 1:
+            tt = torch.tensor([t], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt)
+        return t
+
+    # the reference's default mode (EfficientBayesianBased.java:83,89), measured on the same
+    # views after the primary line's mode unless that already is the default
+    default_mode = None
+    if not args.no_default_mode and not (args.psftype == "OPTIMIZATION_I" and args.lam == 0.006):
+        with make_session("OPTIMIZATION_I") as s2:
+            t2 = timed(s2, 0.006)
+        default_mode = {"psftype": "OPTIMIZATION_I", "lambda": 0.006,
+                        "value": round(nx * ny * nz_g * args.steps / t2 / 1e6, 2),
+                        "ms_per_step": round(t2 / max(args.steps, 1) * 1e3, 3)}
+        torch.cuda.empty_cache()
+    sess = make_session(args.psftype)
+    del imgs, ws
+    torch.cuda.empty_cache()
+    M = sess.fft_dims(0)
+    dt = timed(sess, args.lam)
     ms_per_step = dt / max(args.steps, 1) * 1e3
     n_vox_total = nx * ny * nz_g
     value = n_vox_total * args.steps / dt / 1e6
@@ -238,7 +292,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
+        cpu = cpu_baseline(args, (nx, ny, nz_g))
 
     if rank == 0:
         line = {
@@ -250,15 +304,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32" + ("(fp16 img/w storage)" if args.fp16 else ""),
             "data": "synthetic (seeded bead stacks generated on the GPU, SURVEY 8d)",
-            "config": {"workload": (f"{V}-view {nx}^3" if nx == ny == nz else f"{V}-view {nx}x{ny}x{nz}")
-                                   + f" per GPU (global {nx}x{ny}x{nz_g}), "
-                                   f"{args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}",
+            "config": {"workload": ((f"{V}-view {nx}x{ny}x{nz_g} global, split into {world} z-slabs"
+                                    if args.strong else
+                                    (f"{V}-view {nx}^3" if nx == ny == nz else f"{V}-view {nx}x{ny}x{nz}")
+                                    + f" per GPU (global {nx}x{ny}x{nz_g})")
+                                   + f", {args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}"),
                        "views": V, "volume_xyz": [nx, ny, nz_g], "psf": [args.ksize] * 3,
-                       "fft_dims_xyz": list(M), "parallelism": f"z-slab x{world} (RCCL halo)"},
+                       "fft_dims_xyz": list(M), "local_slabs": args.local_slabs,
+                       "parallelism": f"z-slab x{world} (RCCL halo)"},
+            "default_mode": default_mode,
             "roofline": roofline,
             "roofline_iteration": it_roof,
             "kernel_ms": kernel_ms,
