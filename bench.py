@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--local-slabs", type=int, default=1, help="z-slabs per process (virtual shards)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the global volume --shape (default 1024 1024 512, EFFICIENT_BAYESIAN "
-                         "lambda 0.006 = BASELINE configs[2]) is split into N z-slabs, one per rank")
+                         "lambda 0.006 = BASELINE configs[2]) is split into N slabs along the longer of y and z, one per rank")
     ap.add_argument("--no-default-mode", action="store_true",
                     help="skip the second measurement in the reference default mode (OPTIMIZATION_I, 0.006)")
     a = ap.parse_args()
@@ -159,14 +159,21 @@ def main():
 
     nx, ny, nz = args.shape if args.shape else (args.size,) * 3
     V = args.views
-    if args.strong:      # the global volume is fixed; rank r owns z-slab r of N
+    axis = "z"
+    ny_g = ny
+    if args.strong:      # the global volume is fixed; rank r owns slab r of N along the longer of y, z
         from spim_registration_amd.distributed import slab_range
         nz_g = nz
-        z0, z1 = slab_range(nz_g, world, rank)
-        nz = z1 - z0
+        if ny > nz and world > 1:   # (1024x1024x512: 128 + 24 halo rows per rank, not 64 + 24 planes)
+            axis = "y"
+            o0, o1 = slab_range(ny_g, world, rank)
+            ny = o1 - o0
+        else:
+            o0, o1 = slab_range(nz_g, world, rank)
+            nz = o1 - o0
     else:                # weak scaling: every rank adds an nz-plane slab
         nz_g = nz * world
-        z0 = rank * nz
+        o0 = rank * nz
     imgs, ws, psfs = synthetic.make_views_torch((nz, ny, nx), V, config_id=1 + rank,
                                                 ksize=(args.ksize,) * 3, device=f"cuda:{local}")
     torch.cuda.synchronize()
@@ -179,7 +186,8 @@ def main():
         # a fresh RCCL id per communicator (an id bootstraps one communicator only)
         comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
         s = Session((nx, ny, nz), device=local, nranks=world, rank=rank, comm_id=comm_id,
-                    nz_global=nz_g, z_offset=z0, storage_fp16=args.fp16, local_slabs=args.local_slabs,
+                    nz_global=ny_g if axis == "y" else nz_g, z_offset=o0, slab_axis=axis,
+                    storage_fp16=args.fp16, local_slabs=args.local_slabs,
                     fft_backend=args.backend, fft_pad_policy=args.pad_policy)
         for i, w, k in zip(imgs, ws, psfs):
             s.add_view_device(i.data_ptr(), w.data_ptr(), k)
@@ -212,7 +220,7 @@ def main():
         with make_session("OPTIMIZATION_I") as s2:
             t2 = timed(s2, 0.006)
         default_mode = {"psftype": "OPTIMIZATION_I", "lambda": 0.006,
-                        "value": round(nx * ny * nz_g * args.steps / t2 / 1e6, 2),
+                        "value": round(nx * ny_g * nz_g * args.steps / t2 / 1e6, 2),
                         "ms_per_step": round(t2 / max(args.steps, 1) * 1e3, 3)}
         torch.cuda.empty_cache()
     sess = make_session(args.psftype)
@@ -221,7 +229,7 @@ def main():
     M = sess.fft_dims(0)
     dt = timed(sess, args.lam)
     ms_per_step = dt / max(args.steps, 1) * 1e3
-    n_vox_total = nx * ny * nz_g
+    n_vox_total = nx * ny_g * nz_g
     value = n_vox_total * args.steps / dt / 1e6
 
     # roofline pass: HIP events on the session stream around every kernel class
@@ -292,7 +300,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, (nx, ny, nz_g))
+        cpu = cpu_baseline(args, (nx, ny_g, nz_g))
 
     if rank == 0:
         line = {
@@ -308,14 +316,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" + ("(fp16 img/w storage)" if args.fp16 else ""),
             "data": "synthetic (seeded bead stacks generated on the GPU, SURVEY 8d)",
-            "config": {"workload": ((f"{V}-view {nx}x{ny}x{nz_g} global, split into {world} z-slabs"
+            "config": {"workload": ((f"{V}-view {nx}x{ny_g}x{nz_g} global, split into {world} {axis}-slabs"
                                     if args.strong else
                                     (f"{V}-view {nx}^3" if nx == ny == nz else f"{V}-view {nx}x{ny}x{nz}")
-                                    + f" per GPU (global {nx}x{ny}x{nz_g})")
+                                    + f" per GPU (global {nx}x{ny_g}x{nz_g})")
                                    + f", {args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}"),
-                       "views": V, "volume_xyz": [nx, ny, nz_g], "psf": [args.ksize] * 3,
+                       "views": V, "volume_xyz": [nx, ny_g, nz_g], "psf": [args.ksize] * 3,
                        "fft_dims_xyz": list(M), "local_slabs": args.local_slabs,
-                       "parallelism": f"z-slab x{world} (RCCL halo)"},
+                       "parallelism": f"{axis}-slab x{world} (RCCL halo)"},
             "default_mode": default_mode,
             "roofline": roofline,
             "roofline_iteration": it_roof,

@@ -145,7 +145,15 @@ typedef struct mvd_params {
     int     halo[3];        /* max kernel half size {cx,cy,cz}; 0 = derive from views */
     int     ij_threads;     /* pinned reference thread count for the normImg quirk  */
     int     fft_backend;    /* 0 = fused spectral engine (default), 1 = rocFFT       */
-    int     reserved[7];
+    int     slab_axis;      /* axis the volume is split along (local slabs, devices,  *
+                             * ranks): 0 = z (default), 1 = y, -1 = the longer of y  *
+                             * and z when the volume is split (one rank; else z).    *
+                             * With y, dims is this rank's                           *
+                             * y-range of every z plane and nz_global / z_offset     *
+                             * give the global ny / first y row; the session keeps   *
+                             * its slabs in (x, z, y) order internally (one row      *
+                             * transposition at upload / download)                   */
+    int     reserved[6];
 } mvd_params;
 
 /* fills *p with defaults (local_slabs=1, nranks=1, ij_threads=8, ...) */
@@ -206,7 +214,8 @@ int mvd_apply_mask(mvd_session* h);
 
 /* copy this rank's psi to host (dims of params) */
 int mvd_get_psi(mvd_session* h, float* out);
-/* device pointer of local slab s's psi (valid until mvd_destroy) */
+/* device pointer of local slab s's psi (valid until mvd_destroy); x-fastest
+ * [z][y][x] of the slab, or [y][z][x] when the session splits along y */
 float* mvd_psi_device(mvd_session* h, int slab);
 
 /* padded FFT dims {Mx, My, Mz} of local slab s (info/bench) */

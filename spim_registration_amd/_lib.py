@@ -38,7 +38,8 @@ class MvdParams(C.Structure):
         ("halo", C.c_int * 3),
         ("ij_threads", C.c_int),
         ("fft_backend", C.c_int),
-        ("reserved", C.c_int * 7),
+        ("slab_axis", C.c_int),
+        ("reserved", C.c_int * 6),
     ]
 
 

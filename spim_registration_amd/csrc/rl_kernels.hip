@@ -11,6 +11,8 @@
 //   update    computeNextValue + Tikhonov (f64 sqrt)   MVDeconvolution.java:671-705
 #include "rl_kernels.hpp"
 
+#include <algorithm>
+
 namespace spimdecon {
 
 namespace {
@@ -440,6 +442,26 @@ void launch_mask(float* psi, int64_t n, int nviews, Store st, const void* const*
     else
         hipLaunchKernelGGL(k_mask<1>, dim3(grid_for(n, 256)), dim3(256), 0, s, psi, n, nviews,
                            d_imgs);
+    SD_HIP(hipGetLastError());
+}
+
+// b[y][z][:] = a[z][y][:]; block = 256 threads over one row (grid-stride over rows)
+__global__ __launch_bounds__(256) void k_swap_outer(const float* __restrict__ a, float* __restrict__ b, int64_t nx,
+                                                    int64_t ny, int64_t nz) {
+    const int64_t rows = ny * nz;
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+        const int64_t y = r / nz, z = r % nz;   // destination row r = y * nz + z
+        const float* src = a + (z * ny + y) * nx;
+        float* dst = b + r * nx;
+        for (int64_t x = threadIdx.x; x < nx; x += 256) dst[x] = src[x];
+    }
+}
+
+void launch_swap_outer(const float* a, float* b, int64_t nx, int64_t ny, int64_t nz, hipStream_t s) {
+    const int64_t rows = ny * nz;
+    if (rows == 0 || nx == 0) return;
+    hipLaunchKernelGGL(k_swap_outer, dim3(unsigned(std::min<int64_t>(rows, 256 * 64))), dim3(256), 0, s, a, b, nx,
+                       ny, nz);
     SD_HIP(hipGetLastError());
 }
 

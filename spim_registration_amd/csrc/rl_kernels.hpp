@@ -59,5 +59,9 @@ void launch_mask(float* psi, int64_t n, int nviews, Store st, const void* const*
                  hipStream_t s);
 // float32 -> fp16 conversion (storage mode)
 void launch_to_half(const float* in, void* out, int64_t n, hipStream_t s);
+// Swaps the two outer axes of an x-fastest volume, whole x rows at a time (the
+// y-slab layout of the session): a [nz][ny][nx] -> b[ny][nz][nx], b(y,z) = a(z,y).
+// Coalesced row copies (one block per row pair of 4 rows), nx % 4 == 0 not needed.
+void launch_swap_outer(const float* a, float* b, int64_t nx, int64_t ny, int64_t nz, hipStream_t s);
 
 }  // namespace spimdecon

@@ -43,7 +43,27 @@ void HostBarrier::abort() {
     cv_.notify_all();
 }
 
-Session::Session(const mvd_params& p, const std::vector<int>& devs) : p_(p) {
+// caller's geometry -> internal geometry: a y-split session swaps the roles of y
+// and z (dims and halo), so the engine always slabs its outermost axis
+static mvd_params internal_params(const mvd_params& p, int nslabs, int* axis) {
+    SD_CHECK(p.slab_axis >= -1 && p.slab_axis <= 1, SPIMDECON_ERR_ARG, "slab_axis must be -1, 0 or 1");
+    int a = p.slab_axis;
+    // auto: split the longer of y and z (fewer halo rows per slab); an unsplit volume
+    // keeps its own layout (no transposition)
+    if (a == -1) a = (p.nranks == 1 && nslabs > 1 && p.dims[1] > p.dims[2]) ? 1 : 0;
+    *axis = a;
+    mvd_params q = p;
+    if (a == 1) {
+        std::swap(q.dims[1], q.dims[2]);
+        std::swap(q.halo[1], q.halo[2]);
+    }
+    return q;
+}
+
+Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
+    for (int d = 0; d < 3; ++d) odims_[d] = p0.dims[d];
+    p_ = internal_params(p0, int(std::max<size_t>(devs.size(), 1)) * std::max(p0.local_slabs, 1), &axis_);
+    const mvd_params& p = p_;
     SD_CHECK(p.dims[0] >= 1 && p.dims[1] >= 1 && p.dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
     SD_CHECK(p.local_slabs >= 1, SPIMDECON_ERR_ARG, "local_slabs must be >= 1");
     SD_CHECK(p.nranks >= 1 && p.rank >= 0 && p.rank < p.nranks, SPIMDECON_ERR_ARG, "bad rank");
@@ -154,6 +174,49 @@ void Session::sync_all() {
     }
 }
 
+void Session::load_slab(const float* src, hipMemcpyKind kind, const SlabState& sl, float* dst, DBuf<float>& tmp,
+                        hipStream_t st) const {
+    const int64_t nx = odims_[0], ny = odims_[1], nz = odims_[2];
+    if (axis_ == 0) {
+        SD_HIP(hipMemcpyAsync(dst, src + sl.local_z0 * nx * ny, size_t(sl.n) * 4, kind, st));
+        return;
+    }
+    // y rows [y0, y0 + ys) of every z plane -> tmp [nz][ys][nx] -> dst [ys][nz][nx]
+    const int64_t y0 = sl.local_z0, ys = sl.g.nz;
+    if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
+    SD_HIP(hipMemcpy2DAsync(tmp.p, size_t(ys * nx) * 4, src + y0 * nx, size_t(ny * nx) * 4, size_t(ys * nx) * 4,
+                            size_t(nz), kind, st));
+    launch_swap_outer(tmp.p, dst, nx, ys, nz, st);
+}
+
+void Session::store_slab(const SlabState& sl, const float* src, float* out, DBuf<float>& tmp, hipStream_t st) const {
+    const int64_t nx = odims_[0], ny = odims_[1], nz = odims_[2];
+    if (axis_ == 0) {
+        SD_HIP(hipMemcpyAsync(out + sl.local_z0 * nx * ny, src, size_t(sl.n) * 4, hipMemcpyDeviceToHost, st));
+        return;
+    }
+    const int64_t y0 = sl.local_z0, ys = sl.g.nz;
+    if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
+    launch_swap_outer(src, tmp.p, nx, nz, ys, st);  // [ys][nz][nx] -> [nz][ys][nx]
+    SD_HIP(hipMemcpy2DAsync(out + y0 * nx, size_t(ny * nx) * 4, tmp.p, size_t(ys * nx) * 4, size_t(ys * nx) * 4,
+                            size_t(nz), hipMemcpyDeviceToHost, st));
+}
+
+HostKernel Session::internal_kernel(const HostKernel& k) const {
+    if (axis_ == 0) return k;
+    HostKernel o;
+    const int kx = k.dims[0], ky = k.dims[1], kz = k.dims[2];
+    o.dims[0] = kx;
+    o.dims[1] = kz;
+    o.dims[2] = ky;
+    o.data.resize(k.data.size());
+    for (int z = 0; z < kz; ++z)
+        for (int y = 0; y < ky; ++y)
+            std::copy(k.data.begin() + (int64_t(z) * ky + y) * kx, k.data.begin() + (int64_t(z) * ky + y + 1) * kx,
+                      o.data.begin() + (int64_t(y) * kz + z) * kx);
+    return o;
+}
+
 void Session::add_view(const float* img, const float* weight, const float* k1, const int* kdims,
                        bool device_ptrs) {
     SD_CHECK(img && weight && k1 && kdims, SPIMDECON_ERR_ARG, "null argument");
@@ -166,23 +229,22 @@ void Session::add_view(const float* img, const float* weight, const float* k1, c
     hk.data.assign(k1, k1 + int64_t(kdims[0]) * kdims[1] * kdims[2]);
     // device pointers live on the first device; other groups copy them peer to peer
     const hipMemcpyKind kind = device_ptrs ? hipMemcpyDefault : hipMemcpyHostToDevice;
-    const int64_t plane = p_.dims[0] * p_.dims[1];
     std::vector<std::vector<DBuf<char>>> bufs(slabs_.size());
     for (auto& gr : groups_) {
         DeviceGuard guard(gr.dev);
-        DBuf<float> tmp;
+        DBuf<float> tmp, f32;
         for (int s = gr.s0; s < gr.s1; ++s) {
             SlabState& sl = slabs_[s];
             const size_t esz = store_ == Store::F32 ? 4 : 2;
             for (int which = 0; which < 2; ++which) {
-                const float* src = (which == 0 ? img : weight) + sl.local_z0 * plane;
+                const float* src = which == 0 ? img : weight;
                 DBuf<char> buf(size_t(sl.n) * esz);
                 if (store_ == Store::F32) {
-                    SD_HIP(hipMemcpyAsync(buf.p, src, size_t(sl.n) * 4, kind, gr.stream));
+                    load_slab(src, kind, sl, reinterpret_cast<float*>(buf.p), tmp, gr.stream);
                 } else {
-                    if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
-                    SD_HIP(hipMemcpyAsync(tmp.p, src, size_t(sl.n) * 4, kind, gr.stream));
-                    launch_to_half(tmp.p, buf.p, sl.n, gr.stream);
+                    if (f32.n < size_t(sl.n)) f32.alloc(sl.n);
+                    load_slab(src, kind, sl, f32.p, tmp, gr.stream);
+                    launch_to_half(f32.p, buf.p, sl.n, gr.stream);
                 }
                 bufs[s].push_back(std::move(buf));
             }
@@ -232,9 +294,16 @@ void Session::get_kernels(int view, float* k1, float* k2) const {
 }
 
 void Session::build_spectra() {
+    // kernels in the internal axis order (prepared in the caller's order: the normImg
+    // portions of AdjustInput.java:93-97 follow the original flat order)
+    std::vector<HostKernel> ik1(nviews_), ik2(nviews_);
+    for (int v = 0; v < nviews_; ++v) {
+        ik1[v] = internal_kernel(k1_[v]);
+        ik2[v] = internal_kernel(k2_[v]);
+    }
     int h[3] = {0, 0, 0};
     for (int v = 0; v < nviews_; ++v)
-        for (int d = 0; d < 3; ++d) h[d] = std::max(h[d], k1_[v].dims[d] / 2);
+        for (int d = 0; d < 3; ++d) h[d] = std::max(h[d], ik1[v].dims[d] / 2);
     for (int d = 0; d < 3; ++d) halo_[d] = std::max(h[d], p_.halo[d]);
     const int total_slabs = int(slabs_.size()) * p_.nranks;
     for (auto& sl : slabs_) {
@@ -283,7 +352,7 @@ void Session::build_spectra() {
             sl.k2spec.clear();
             for (int v = 0; v < nviews_; ++v) {
                 for (int which = 0; which < 2; ++which) {
-                    const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
+                    const HostKernel& hk = which == 0 ? ik1[v] : ik2[v];
                     kd.alloc(hk.data.size());
                     SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
                     DBuf<float> spec(rf);
@@ -313,7 +382,7 @@ void Session::build_spectra() {
             if (sl.kcompact) work.alloc(ne);
             for (int v = 0; v < nviews_; ++v) {
                 for (int which = 0; which < 2; ++which) {
-                    const HostKernel& hk = which == 0 ? k1_[v] : k2_[v];
+                    const HostKernel& hk = which == 0 ? ik1[v] : ik2[v];
                     kd.alloc(hk.data.size());
                     SD_HIP(hipMemcpyAsync(kd.p, hk.data.data(), kd.bytes(), hipMemcpyHostToDevice, stream_));
                     DBuf<float2> spec;
@@ -357,13 +426,13 @@ double Session::init_psi(const float* psi_or_null) {
         }
     }
     if (psi_or_null) {
-        const int64_t plane = p_.dims[0] * p_.dims[1];
         for (auto& sl : slabs_) {
             DeviceGuard guard(groups_[sl.grp].dev);
             hipStream_t st = groups_[sl.grp].stream;
-            SD_HIP(hipMemcpyAsync(sl.psi, psi_or_null + sl.local_z0 * plane, size_t(sl.n) * 4,
-                                  hipMemcpyHostToDevice, st));
+            DBuf<float> tmp;
+            load_slab(psi_or_null, hipMemcpyHostToDevice, sl, sl.psi, tmp, st);
             launch_clamp_min(sl.psi, sl.n, st);
+            SD_HIP(hipStreamSynchronize(st));
         }
     } else {
         // FirstIteration + fuseFirstIteration (MVDeconvolution.java:192-235)
@@ -828,13 +897,12 @@ void Session::apply_mask() {
 void Session::get_psi(float* out) {
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
     SD_CHECK(out, SPIMDECON_ERR_ARG, "null output");
-    const int64_t plane = p_.dims[0] * p_.dims[1];
     for (auto& sl : slabs_) {
         DeviceGuard guard(groups_[sl.grp].dev);
-        SD_HIP(hipMemcpyAsync(out + sl.local_z0 * plane, sl.psi, size_t(sl.n) * 4,
-                              hipMemcpyDeviceToHost, groups_[sl.grp].stream));
+        DBuf<float> tmp;
+        store_slab(sl, sl.psi, out, tmp, groups_[sl.grp].stream);
+        SD_HIP(hipStreamSynchronize(groups_[sl.grp].stream));
     }
-    sync_all();
 }
 
 float* Session::psi_device(int slab) {

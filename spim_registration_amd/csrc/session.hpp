@@ -118,6 +118,13 @@ public:
 
 private:
     void build_spectra();
+    // original-layout volume (this rank's part, odims_) <-> slab sl in the internal
+    // layout (f32, sl.n floats on the slab's device); y-split sessions transpose rows
+    void load_slab(const float* src, hipMemcpyKind kind, const SlabState& sl, float* dst, DBuf<float>& tmp,
+                   hipStream_t st) const;
+    void store_slab(const SlabState& sl, const float* src, float* out, DBuf<float>& tmp, hipStream_t st) const;
+    // kernel k in the internal axis order (y and z swapped for y-split sessions)
+    HostKernel internal_kernel(const HostKernel& k) const;
     static float* buf_ptr(SlabState& sl, bool a, int backend);
     size_t plane_floats() const;
     // halo exchange of one buffer (C1/Ra when buffer_a) among the slabs of group gi and,
@@ -138,7 +145,9 @@ private:
     void tstart(int cls, hipStream_t st = nullptr);
     void tstop(hipStream_t st = nullptr);
 
-    mvd_params p_{};
+    mvd_params p_{};        // internal geometry (dims / halo with y and z swapped when axis_ == 1)
+    int64_t odims_[3] = {0, 0, 0};  // this rank's volume in the caller's layout {nx, ny, nz}
+    int axis_ = 0;          // slab axis: 0 = z, 1 = y (mvd_params.slab_axis)
     int backend_ = 0;  // 0 = fused spectral engine, 1 = rocFFT (mvd_params.fft_backend)
     Store store_ = Store::F32;
     std::vector<DevGroup> groups_;

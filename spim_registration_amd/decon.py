@@ -140,16 +140,17 @@ class Session:
 
     def __init__(self, dims_xyz, device=0, local_slabs=1, nranks=1, rank=0, comm_id=None,
                  nz_global=None, z_offset=0, storage_fp16=False, ij_threads=8, halo=None,
-                 fft_backend="engine", fft_pad_policy="auto", devices=None):
+                 fft_backend="engine", fft_pad_policy="auto", devices=None, slab_axis="auto"):
         """``devices``: several GPUs of this process (``mvd_create_devices``; the
         reference's ``deviceList``, MVDeconFFT.java:58-64) -- the volume is split into
-        len(devices) * local_slabs z-slabs and one ``run`` drives all of them."""
+        len(devices) * local_slabs slabs and one ``run`` drives all of them.
+        ``slab_axis``: "z", "y" or "auto" (the longer of y and z; z for several ranks)."""
         self.lib = _lib.load()
         p = _lib.MvdParams()
         self.lib.mvd_params_default(C.byref(p))
         for d in range(3):
             p.dims[d] = int(dims_xyz[d])
-        p.nz_global = int(nz_global if nz_global is not None else dims_xyz[2])
+        p.nz_global = int(nz_global) if nz_global is not None else 0   # 0: this volume (slab axis)
         p.z_offset = int(z_offset)
         p.device = int(device)
         p.local_slabs = int(local_slabs)
@@ -161,6 +162,7 @@ class Session:
         p.ij_threads = int(ij_threads)
         p.fft_backend = {"engine": 0, "rocfft": 1}[fft_backend]
         p.fft_pad_policy = {"auto": 0, "fast": 1, "smooth": 2}[fft_pad_policy]
+        p.slab_axis = {"z": 0, "y": 1, "auto": -1}[slab_axis]
         if halo is not None:
             for d in range(3):
                 p.halo[d] = int(halo[d])

@@ -126,6 +126,49 @@ def test_device_groups_reject_bad_arguments(gpu):
     with pytest.raises(SpimDeconError):
         Session((16, 16, 16), devices=[0, 0], fft_backend="rocfft")
     with pytest.raises(SpimDeconError):
-        Session((16, 16, 3), devices=[0, 0], local_slabs=2)     # 4 slabs > 3 planes
+        Session((16, 16, 3), devices=[0, 0], local_slabs=2, slab_axis="z")     # 4 slabs > 3 planes
     with pytest.raises(SpimDeconError):
         Session((16, 16, 16), devices=[0, -1])
+
+
+# y-split sessions (mvd_params.slab_axis = 1): the engine slabs its outermost axis, so
+# the session keeps (x, z, y) rows internally; ny > nz here, so "auto" picks y
+Y_SHAPE = (20, 60, 248)        # [z, y, x]
+
+
+@pytest.mark.parametrize("devices,slabs", [(None, 2), ([0, 0], 1), ([0, 0, 0], 2)])
+def test_y_split_matches_z_split_and_oracle(gpu, devices, slabs):
+    imgs, ws, ks, _ = synthetic.make_views(Y_SHAPE, 3, config_id=13, ksize=(9, 7, 5), weights="blend",
+                                           partial=True, bead_density=1.0 / 6 ** 3)
+    out = {}
+    for axis in ("z", "y", "auto"):
+        kw = dict(local_slabs=slabs if axis != "z" else 1, slab_axis=axis)
+        if devices and axis != "z":
+            kw["devices"] = devices
+        out[axis] = run_session(imgs, ws, ks, psftype=PSFTYPE.EFFICIENT_BAYESIAN, **kw)
+    assert out["y"][2] == [2] * (slabs * len(devices or [0]))   # x tiles ran on the y slabs
+    assert rel_l2(out["y"][0], out["z"][0]) < 1e-5
+    assert np.array_equal(out["auto"][0], out["y"][0])
+    np.testing.assert_allclose(out["y"][1], out["z"][1], rtol=1e-4)
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.EFFICIENT_BAYESIAN, 3, 0.006)
+    assert rel_l2(out["y"][0], res.psi) < TOL
+    assert ((out["y"][0] == 0) == (res.psi == 0)).all()
+
+
+def test_y_split_fp16_initial_image_and_kernels(gpu):
+    imgs, ws, ks, _ = synthetic.make_views(Y_SHAPE, 2, config_id=14, ksize=(5, 9, 3), weights="blend",
+                                           bead_density=1.0 / 6 ** 3)
+    init = imgs[0].copy()
+    out = []
+    for axis in ("z", "y"):
+        with Session(Y_SHAPE[::-1], storage_fp16=True, local_slabs=2 if axis == "y" else 1, slab_axis=axis) as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.OPTIMIZATION_I)
+            k1, k2 = s.get_kernels(1, ks[1].shape)          # the caller's axis order
+            s.init_psi(init)
+            s.run(3, 0.006)
+            out.append((s.get_psi(), k1, k2))
+    assert rel_l2(out[1][0], out[0][0]) < 1e-5
+    np.testing.assert_array_equal(out[1][1], out[0][1])
+    np.testing.assert_array_equal(out[1][2], out[0][2])
