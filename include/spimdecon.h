@@ -105,6 +105,14 @@ int32_t convolve_127(float* image, const float* kernelX, const float* kernelY, c
                      int imageW, int imageH, int imageD, int32_t convolveX, int32_t convolveY,
                      int32_t convolveZ, int outofbounds, float outofboundsvalue, int devCUDA);
 
+/* CPU variant declared by the same interface (CUDASeparableConvolution.java:21) and
+ * never called by the reference.  There is no CPU path here: returns
+ * SPIMDECON_ERR_DEVICE and leaves the image unchanged (a `void` JNA binding ignores
+ * the status; spimdecon_last_error() holds the message). */
+int     convolutionCPU(float* image, const float* kernelX, const float* kernelY, const float* kernelZ,
+                       int kernelRX, int kernelRY, int kernelRZ, int imageW, int imageH, int imageD,
+                       int outofbounds, float outofboundsvalue);
+
 /* ======================================================================
  * 4. Kernel preparation -- spim/process/fusion/deconvolution/MVDeconFFT.java:162-303
  *    (MVDeconInput.init order, AdjustInput.normImg quirk with ij_threads).
@@ -293,6 +301,19 @@ int spim_dog_compute(const float* img, const int64_t* dims, const spim_dog_param
 int spim_dog_interest_points(const float* img, const int64_t* dims, const spim_dog_params* p,
                              float* dog_out, spim_interest_point* out, int64_t max_out,
                              int64_t* nout);
+
+/* Interest-point list files (InterestPointList.java:66-100 save, :178-220 load):
+ * <base_dir>/<file>.ip.txt (base_dir may be NULL or ""; missing parent directories
+ * are created), header "id\tx\ty\tz", one line per point with the doubles printed
+ * as Java's Double.toString.  ids (may be NULL: id = index, as ProcessDOG assigns
+ * them) are written / read beside pos.  Load: *nout = points in the file; at most
+ * max_out are stored (intensity / is_max are 0: the file holds positions only). */
+int spim_save_interest_points(const char* base_dir, const char* file, const spim_interest_point* pts,
+                              const int32_t* ids, int64_t n);
+int spim_load_interest_points(const char* base_dir, const char* file, spim_interest_point* out,
+                              int32_t* ids, int64_t max_out, int64_t* nout);
+/* Java Double.toString of d into out (cap bytes incl. the terminator) */
+int spim_java_double_to_string(double d, char* out, int cap);
 
 /* ======================================================================
  * 7. Deconvolution input preparation --

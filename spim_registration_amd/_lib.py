@@ -132,6 +132,13 @@ SIGNATURES = {
                                    _i64, _pi64]),
     "spim_dog_interest_points": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf,
                                            C.POINTER(InterestPointC), _i64, _pi64]),
+    "spim_save_interest_points": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(InterestPointC),
+                                            C.POINTER(C.c_int32), C.c_int64]),
+    "spim_load_interest_points": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(InterestPointC),
+                                            C.POINTER(C.c_int32), C.c_int64, _pi64]),
+    "spim_java_double_to_string": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
+    "convolutionCPU": (C.c_int, [_pf, _pf, _pf, _pf, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, C.c_float]),
     "spim_input_params_default": (None, [C.POINTER(InputParams)]),
     "spim_fusion_params_default": (None, [C.POINTER(FusionParams)]),
     "spim_psf_transformed_size": (C.c_int, [_pi64, _pd, _pi64, _pd]),

@@ -31,6 +31,7 @@ struct PlanEntry {
     std::unique_ptr<FftPlan3D> fft;
     DBuf<float> buf;
     std::vector<CachedSpectrum> spectra;
+    uint64_t stamp = 0;  // last use (LRU eviction beyond kMaxPlans)
 };
 
 struct DeviceCtx {
@@ -51,6 +52,10 @@ DeviceCtx& device_ctx(int dev) {
 }
 
 constexpr size_t kMaxSpectra = 16;
+// block shapes cached per device: a long-lived JVM that walks datasets with different
+// block sizes would otherwise keep a plan, a padded work block and up to kMaxSpectra
+// kernel spectra per shape forever; the least recently used is dropped
+constexpr size_t kMaxPlans = 4;
 
 const float* spectrum_for(PlanEntry& pe, DeviceCtx& ctx, const SlabGeom& g, const PadDims& pd,
                           const float* kernel, const int kd[3]) {
@@ -113,7 +118,16 @@ void fft_convolve_block(float* im, const int* imDim, const float* kernel, const 
     pd.M[0] = nx;
     pd.M[1] = ny;
     pd.M[2] = nz;
-    PlanEntry& pe = ctx.plans[{nx, ny, nz}];
+    const std::array<int64_t, 3> key{nx, ny, nz};
+    if (!ctx.plans.count(key) && ctx.plans.size() >= kMaxPlans) {
+        auto lru = ctx.plans.begin();
+        for (auto it = ctx.plans.begin(); it != ctx.plans.end(); ++it)
+            if (it->second.stamp < lru->second.stamp) lru = it;
+        SD_HIP(hipStreamSynchronize(ctx.stream));
+        ctx.plans.erase(lru);
+    }
+    PlanEntry& pe = ctx.plans[key];
+    pe.stamp = ++ctx.clock;
     if (!pe.fft) {
         pe.fft.reset(new FftPlan3D());
         pe.fft->create(pd, ctx.stream);

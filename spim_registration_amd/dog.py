@@ -95,3 +95,61 @@ def simple_peaks(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, 
 def peaks_array(points) -> np.ndarray:
     """[(x, y, z)] int array of interest-point locations."""
     return np.array([[int(c) for c in p.location] for p in points], np.int64).reshape(-1, 3)
+
+
+class InterestPointList:
+    """spim/fiji/spimdata/interestpoints/InterestPointList.java:19-220 (interest points
+    only; correspondences belong to registration, out of scope).  ``base_dir`` + ``file``
+    name the list as in the XML; the text file is ``<base_dir>/<file>.ip.txt``, written
+    and read by the library (``spim_save_interest_points`` / ``spim_load_interest_points``)."""
+
+    def __init__(self, base_dir, file):
+        self.base_dir = str(base_dir) if base_dir is not None else ""
+        self.file = str(file)
+        self.interest_points: list[InterestPoint] | None = None
+        self.parameters = ""
+
+    def get_interest_points_ext(self):
+        return ".ip.txt"
+
+    def set_interest_points(self, pts):
+        self.interest_points = list(pts)
+
+    def get_interest_points(self):
+        return self.interest_points
+
+    def save_interest_points(self) -> bool:
+        """saveInterestPoints (:66-100); False without a list, like the reference."""
+        if self.interest_points is None:
+            return False
+        n = len(self.interest_points)
+        arr = (_lib.InterestPointC * max(n, 1))()
+        ids = (C.c_int32 * max(n, 1))()
+        for i, p in enumerate(self.interest_points):
+            for d in range(3):
+                arr[i].pos[d] = float(p.location[d])
+            ids[i] = int(p.id)
+        check(_lib.load().spim_save_interest_points(self.base_dir.encode(), self.file.encode(), arr, ids, n))
+        return True
+
+    def load_interest_points(self) -> bool:
+        """loadInterestPoints (:178-220)."""
+        lib = _lib.load()
+        n = C.c_int64(0)
+        check(lib.spim_load_interest_points(self.base_dir.encode(), self.file.encode(), None, None, 0,
+                                            C.byref(n)))
+        cap = max(int(n.value), 1)
+        arr = (_lib.InterestPointC * cap)()
+        ids = (C.c_int32 * cap)()
+        check(lib.spim_load_interest_points(self.base_dir.encode(), self.file.encode(), arr, ids, cap,
+                                            C.byref(n)))
+        self.interest_points = [InterestPoint(int(ids[i]), (arr[i].pos[0], arr[i].pos[1], arr[i].pos[2]))
+                                for i in range(int(n.value))]
+        return True
+
+
+def java_double_to_string(d: float) -> str:
+    """Double.toString as written into .ip.txt files (library formatter)."""
+    buf = C.create_string_buffer(64)
+    check(_lib.load().spim_java_double_to_string(float(d), buf, 64))
+    return buf.value.decode()

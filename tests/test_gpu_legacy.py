@@ -75,3 +75,50 @@ def test_separable_convolve_bad_device(gpu):
     k = np.zeros(7, np.float32)
     k[3] = 1
     assert cuda.convolve_7(im, k, k, k, 3, 3, 3, True, True, True, 0, 0.0, -1) is False
+
+
+def test_convolution3dfft_concurrent_threads(gpu):
+    """MVDeconFFT.java:424-446 calls convolution3DfftCUDAInPlace from one Java thread
+    per device at once: the export serialises per device (mutex, stream, caches) and
+    every concurrent call returns its own block's convolution.  ctypes releases the
+    GIL around the foreign call, so the calls really overlap."""
+    import threading
+    rng = np.random.default_rng(3)
+    shapes = [(32, 30, 28), (24, 26, 20), (32, 30, 28), (17, 23, 29)] * 3
+    blks = [rng.random(s).astype(np.float32) for s in shapes]
+    ks = [rng.random((5, 7, 9)).astype(np.float32) for _ in shapes]
+    cuda = legacy.CUDAFourierConvolution()
+    outs = [b.copy() for b in blks]
+    errs = []
+
+    def work(i):
+        try:
+            cuda.convolution3DfftCUDAInPlace(outs[i].reshape(-1), list(shapes[i]), ks[i], [5, 7, 9], 0)
+        except Exception as e:      # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(blks))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    for b, k, o in zip(blks, ks, outs):
+        assert rel_l2(o, ref.circular_convolve_block(b, k)) < 1e-6
+
+
+def test_convolution3dfft_plan_cache_bounded(gpu):
+    """the per-device plan cache keeps at most 4 block shapes, so walking
+    many block sizes does not grow device memory without bound."""
+    f = legacy.CUDAStandardFunctions()
+    cuda = legacy.CUDAFourierConvolution()
+    rng = np.random.default_rng(4)
+    k = rng.random((3, 3, 3)).astype(np.float32)
+    free = []
+    for i in range(12):
+        s = (96 + 2 * i, 96, 96)
+        blk = rng.random(s).astype(np.float32)
+        cuda.convolution3DfftCUDAInPlace(blk.reshape(-1), list(s), k, [3, 3, 3], 0)
+        free.append(f.getFreeMemDeviceCUDA(0))
+    # after the cache is full (4 shapes), free memory stops falling by a block's worth per call
+    assert min(free[6:]) > free[5] - 64 * 2 ** 20, [x >> 20 for x in free]
