@@ -302,6 +302,12 @@ int spim_dog_interest_points(const float* img, const int64_t* dims, const spim_d
                              float* dog_out, spim_interest_point* out, int64_t max_out,
                              int64_t* nout);
 
+/* The two DoG calls above keep a per-device workspace between calls (the
+ * intermediate Gaussians, candidate lists; ~12 B per voxel of the largest view seen)
+ * instead of allocating per call; this frees it.  No reference counterpart (the
+ * reference's CUDA library allocates per call, CUDASeparableConvolution.java:13-21). */
+int spim_dog_release_workspace(int device);
+
 /* Interest-point list files (InterestPointList.java:66-100 save, :178-220 load):
  * <base_dir>/<file>.ip.txt (base_dir may be NULL or ""; missing parent directories
  * are created), header "id\tx\ty\tz", one line per point with the doubles printed

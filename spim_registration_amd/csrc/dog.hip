@@ -10,19 +10,29 @@
 //   mpicbg/spim/segmentation/InteractiveIntegral.java:360-468     findPeaks / isSpecialPoint
 //   spim/process/fusion/FusionHelper.java:176-234                 normalizeImage
 //
-// Data flow of one DoG (all HBM-resident, 5 streaming passes):
-//   x-pass  img --(normalise on the fly)--> G1x, G2x      (both sigmas from one read)
-//   y-pass  G1x -> G1xy, G2x -> G2xy
-//   z-pass  G1xy, G2xy -> dog = (G2 - G1) * 1/(k-1)       (subtraction fused)
-//   peaks   26-neighbour extremum test + order-preserving compaction
-// Accumulation order per pass = tap order in float32 (matches the oracle bit for bit).
+// Data flow of one DoG (all HBM-resident, two streaming passes for Gaussians of 7 / 15 /
+// 31 taps -- the ProcessDOG sigmas):
+//   k_dog_xy  img --(normalise on the fly)--> x then y Gaussians of both sigmas -> G12
+//   k_dog_z   G12 -> z Gaussians -> dog = (G2 - G1) * 1/(k-1) -> 26-neighbour test ->
+//             candidate append; device radix sort into the reference's order
+// (63 / 127 taps: the separate x / y / z passes, then a candidate pass over the DoG.)
+// Accumulation order = tap order in float32 (matches the oracle bit for bit).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
 
 namespace spimdecon {
+
+// dog_sort.hip
+size_t peak_sort_temp_bytes(int64_t n, int end_bit);
+void peak_sort(void* tmp, size_t tmp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+               uint32_t* vout, int64_t n, int end_bit, hipStream_t s);
 
 namespace {
 
@@ -329,15 +339,315 @@ __global__ __launch_bounds__(kSepTX * kSepTY) void k_sep_yz(Dims3 d, const float
     }
 }
 
+// ---------------------------------------------------------------- fused DoG (the ProcessDOG path)
+// Two streaming kernels replace the three separable passes and the two peak passes:
+//   k_dog_xy  img --normalise--> x, then y Gaussians of both sigmas -> G12 (float2 per voxel)
+//   k_dog_z   G12 -> z Gaussians -> DoG (stored only when asked) -> 26-neighbour test ->
+//             candidates appended as (key, record); a device radix sort on the key
+//             (x % T) << 40 | flat restores the reference order (dog_sort.hip).
+// Every output keeps the float32 tap order of k_sep_x / k_sep_yz (packed mul, then
+// packed add, no contraction): the DoG image is bit-identical to the separate passes.
+// HBM per voxel: 4 B read + 8 B write (xy), 8 B read (+ 4 B DoG write) (z) -- 20-24 B
+// against 48 B for the separate passes plus two re-reads of the DoG by the peak passes.
+constexpr int kDxyTX = 64;   // xy tile: outputs along x (TY along y: template)
+constexpr int kDxySeg = 8;   // x outputs per thread in the x phase (register window)
+constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave per row, the
+                             // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
+constexpr int kDzPD = 3;     // planes loaded ahead of use
+constexpr int kDzChunk = 64; // DoG planes per block (the window adds KW - 1 + 2 loads)
+
+__device__ __forceinline__ int mirror32(int i, int n) {
+    bool o;
+    return ext_index32(i, n, OOB_MIRROR, o);
+}
+
+// LDS writes visible to the block, without the release fence of __syncthreads (which
+// would also wait for the planes loaded ahead)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int KW, int TY>
+__global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
+                                                const float2* __restrict__ ky, float2* __restrict__ g12,
+                                                const float* __restrict__ mm) {
+    constexpr int R = KW / 2;
+    constexpr int IW = kDxyTX + KW - 1;          // staged input columns
+    constexpr int IP = (IW + 3) / 4 * 4;         // pitch: 16-B aligned rows
+    constexpr int IH = TY + KW - 1;              // staged input rows
+    constexpr int NSEG = kDxyTX / kDxySeg;
+    constexpr int WX = kDxySeg + KW - 1;
+    constexpr int OY = TY / 4;                   // y outputs per thread (4 runs per column)
+    constexpr int WY = OY + KW - 1;
+    __shared__ __attribute__((aligned(16))) float sin_[IH * IP];
+    __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxyTX];
+    const int nx = int(d.nx), ny = int(d.ny);
+    const int x0 = int(blockIdx.x) * kDxyTX, y0 = int(blockIdx.y) * TY;
+    const uint32_t plane = uint32_t(blockIdx.z) * uint32_t(ny) * uint32_t(nx);
+    const int t = threadIdx.x;
+    // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
+    bool norm = false;
+    float mn = 0.0f, diff = 1.0f;
+    if (mm) {
+        mn = mm[0];
+        diff = __fsub_rn(mm[1], mn);
+        norm = !(isnan(diff) || isinf(diff) || diff == 0.0f);
+    }
+    // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
+    // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
+    // load; every load in flight before the first use (a load per round trip exposed
+    // the HBM latency ~19 times per tile)
+    constexpr int RPT = 256 / IW;                // rows staged per pass
+    constexpr int IPC = 256 / RPT;               // threads per row (>= IW)
+    constexpr int NE = (IH + RPT - 1) / RPT;     // rows per thread
+    const int col = t % IPC, r0 = t / IPC;
+    const bool cact = col < IW && r0 < RPT;
+    const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
+    float v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int row = min(r0 + RPT * e, IH - 1);
+        v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
+    }
+    if (cact) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int row = r0 + RPT * e;
+            if (row >= IH) break;
+            sin_[row * IP + col] = norm ? __fdiv_rn(__fsub_rn(v[e], mn), diff) : v[e];
+        }
+    }
+    __syncthreads();
+    // x phase: every staged row, kDxySeg outputs per thread from a window of WX values
+    for (int it = t; it < IH * NSEG; it += 256) {
+        const int row = it / NSEG, seg = it - row * NSEG;
+        const float* src = sin_ + row * IP + seg * kDxySeg;
+        float w[WX];
+#pragma unroll
+        for (int i = 0; i < WX; ++i) w[i] = src[i];
+        dg_v2 acc[kDxySeg];
+#pragma unroll
+        for (int o = 0; o < kDxySeg; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+            const dg_v2 k = dg_v2{kx[j].x, kx[j].y};
+#pragma unroll
+            for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
+        }
+        float2* dst = sx + row * kDxyTX + seg * kDxySeg;
+#pragma unroll
+        for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
+    }
+    __syncthreads();
+    // y phase: column c, OY consecutive outputs
+    const int c = t & (kDxyTX - 1), run = t / kDxyTX;
+    const int x = x0 + c;
+    if (x >= nx) return;
+    dg_v2 w[WY];
+#pragma unroll
+    for (int i = 0; i < WY; ++i) {
+        const float2 v = sx[(run * OY + i) * kDxyTX + c];
+        w[i] = dg_v2{v.x, v.y};
+    }
+    dg_v2 acc[OY];
+#pragma unroll
+    for (int o = 0; o < OY; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        const dg_v2 k = dg_v2{ky[j].x, ky[j].y};
+#pragma unroll
+        for (int o = 0; o < OY; ++o) acc[o] = acc[o] + w[o + j] * k;
+    }
+#pragma unroll
+    for (int o = 0; o < OY; ++o) {
+        const int y = y0 + run * OY + o;
+        if (y < ny) g12[plane + uint32_t(y) * uint32_t(nx) + uint32_t(x)] = make_float2(acc[o].x, acc[o].y);
+    }
+}
+
+struct PeakOut {
+    int32_t x, y, z;
+    float intensity;
+    int32_t is_min, is_max;
+};
+
+// candidate sink: unordered append of (key, record); count may exceed cap (the host reruns)
+struct PeakSink {
+    float minv;
+    int want_min, want_max, T;
+    uint64_t* keys;
+    uint32_t* vals;
+    PeakOut* recs;
+    unsigned* count;
+    unsigned cap;
+};
+
+// one wave-wide append; every lane of the wave must call it
+__device__ __forceinline__ void sink_append(const PeakSink& pk, bool flag, int x, int y, int z, uint64_t flat,
+                                            float c, int sp) {
+    const unsigned long long bal = __ballot(flag);
+    if (bal == 0ull) return;
+    const int lane = int(threadIdx.x & 63);
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(pk.count, unsigned(__popcll(bal)));
+    base = unsigned(__shfl(int(base), 0, 64));
+    const unsigned pos = base + unsigned(__popcll(bal & ((1ull << lane) - 1ull)));
+    if (flag && pos < pk.cap) {
+        pk.keys[pos] = (uint64_t(x % pk.T) << 40) | flat;
+        pk.vals[pos] = pos;
+        PeakOut o;
+        o.x = x;
+        o.y = y;
+        o.z = z;
+        o.intensity = fabsf(c);
+        o.is_min = sp == 1;
+        o.is_max = sp == 2;
+        pk.recs[pos] = o;
+    }
+}
+
+// z Gaussians + DoG + peak test over one column box and one chunk of planes.  Each
+// thread keeps its column's window of KW planes (+ kDzPD loaded ahead) of (G1, G2) in
+// registers, rotating by unrolling; the DoG planes go through a 4-plane LDS ring.  The
+// 26-neighbour test is min / max of the 3x3x3 box (the box includes the centre, so
+// "all neighbours >= c" <=> box min >= c); a plane holding a NaN takes the
+// reference's comparison loop instead (NaN compares false).
+template <int KW, int BY>
+__global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
+                                                         const float2* __restrict__ kz, float scale, int zc_len,
+                                                         float* __restrict__ dog, PeakSink pk) {
+    constexpr int R = KW / 2;
+    constexpr int NW = KW + kDzPD;
+    __shared__ float Dr[4][BY][kDzBX];
+    __shared__ int nanq[4];
+    const int t = threadIdx.x, tx = t & (kDzBX - 1), ty = t / kDzBX;
+    const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
+    const int X0 = int(blockIdx.x) * (kDzBX - 2), Y0 = int(blockIdx.y) * (BY - 2);
+    const int x = X0 + tx, y = Y0 + ty;
+    const bool valid = x < nx && y < ny;
+    const int z0 = int(blockIdx.z) * zc_len, z1 = min(nz, z0 + zc_len);
+    const int qa = max(z0 - 1, 0), qb = min(z1 + 1, nz);   // DoG planes computed
+    const int len = qb - qa + KW - 1;                       // source planes loaded
+    const int tlo = max(z0, 1), thi = min(z1, nz - 1);      // centre planes tested
+    const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
+    const uint32_t col = valid ? uint32_t(y) * uint32_t(nx) + uint32_t(x) : 0u;
+    // DoG store ownership: the tile's tested columns, plus the volume's outer ring
+    const bool lastx = blockIdx.x == gridDim.x - 1, lasty = blockIdx.y == gridDim.y - 1;
+    const bool own = valid && tx >= (blockIdx.x == 0 ? 0 : 1) && (lastx || tx < kDzBX - 1) &&
+                     ty >= (blockIdx.y == 0 ? 0 : 1) && (lasty || ty < BY - 1);
+    const bool inner = valid && tx >= 1 && tx < kDzBX - 1 && ty >= 1 && ty < BY - 1 && x <= nx - 2 &&
+                       y <= ny - 2;
+    if (t < 4) nanq[t] = -1;
+    __syncthreads();
+    // unconditional loads (columns outside the volume read column 0; the tail re-reads
+    // the last plane): no branch merge, so they stay in flight kDzPD planes ahead
+    auto ld = [&](int i) -> float2 {
+        return g12[uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride + col];
+    };
+    // step s: window = source planes s .. s + KW - 1 in slots (s + j) % NW, DoG plane
+    // q = qa + s; the step count is padded to whole NW rotations (padded steps test and
+    // store nothing), so the unrolled body has no exits
+    float2 w[NW];
+#pragma unroll
+    for (int p = 0; p < NW - 1; ++p) w[p] = ld(p);
+    const int nsteps = (qb - qa + NW - 1) / NW * NW;
+    float mnA = 0.f, mxA = 0.f, mnB = 0.f, mxB = 0.f, mnC = 0.f, mxC = 0.f, dB = 0.f, dC = 0.f;
+    int nanhist = 0;   // bit k: the block's DoG plane q - k holds a NaN
+    const uint32_t dog_bytes = dog ? pstride * 4u : 0u;
+    for (int sb = 0; sb < nsteps; sb += NW) {
+#pragma unroll
+        for (int ph = 0; ph < NW; ++ph) {
+            const int st = sb + ph;
+            w[(ph + NW - 1) % NW] = ld(st + NW - 1);
+            dg_v2 acc = {0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {   // tap order kept
+                const float2 v = w[(ph + j) % NW];
+                acc = acc + dg_v2{v.x, v.y} * dg_v2{kz[j].x, kz[j].y};
+            }
+            const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
+            const int q = qa + st;
+            {   // the DoG store: a buffer store, dropped (out of range) unless owned
+                const bool st_ok = own && q >= z0 && q < z1;
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    dog + (dog ? size_t(min(q, nz - 1)) * pstride : 0), 0, int(dog_bytes), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd,
+                                                      int(st_ok ? col * 4u : 0x80000000u), 0, 0);
+            }
+            const int slot = q & 3;
+            Dr[slot][ty][tx] = dv;
+            if (__ballot(dv != dv) != 0ull && tx == 0) nanq[slot] = q;
+            lds_barrier();
+            nanhist = ((nanhist << 1) | (nanq[slot] == q ? 1 : 0)) & 7;
+            mnA = mnB; mxA = mxB; mnB = mnC; mxB = mxC;
+            dB = dC;
+            dC = dv;
+            if (inner) {
+                float m = dv, M = dv;
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        if (dy == 0 && dx == 0) continue;
+                        const float v = Dr[slot][ty + dy][tx + dx];
+                        m = fminf(m, v);
+                        M = fmaxf(M, v);
+                    }
+                mnC = m;
+                mxC = M;
+            }
+            const int zc = q - 1;   // centre plane of the test
+            if (zc >= tlo && zc < thi) {
+                int sp = 0;
+                const float c = dB;
+                if (inner && !(fabsf(c) < pk.minv)) {
+                    bool ge, le;
+                    if (nanhist == 0) {
+                        ge = fminf(fminf(mnA, mnB), mnC) >= c;
+                        le = fmaxf(fmaxf(mxA, mxB), mxC) <= c;
+                    } else {
+                        ge = le = true;
+                        for (int dz = -1; dz <= 1; ++dz)
+                            for (int dy = -1; dy <= 1; ++dy)
+                                for (int dx = -1; dx <= 1; ++dx) {
+                                    if (dz == 0 && dy == 0 && dx == 0) continue;
+                                    const float v = Dr[(zc + dz) & 3][ty + dy][tx + dx];
+                                    ge &= v >= c;
+                                    le &= v <= c;
+                                }
+                    }
+                    // "this mixup is intended" (InteractiveIntegral.isSpecialPoint)
+                    sp = ge ? 2 : (le ? 1 : 0);
+                }
+                const bool flag = (sp == 2 && pk.want_max) || (sp == 1 && pk.want_min);
+                sink_append(pk, flag, x, y, zc, uint64_t(zc) * pstride + col, c, sp);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in, int64_t n,
                                                     float* __restrict__ partial) {
     __shared__ float smn[kBlock / 64], smx[kBlock / 64];
     float mn = INFINITY, mx = -INFINITY;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n;
-         i += int64_t(gridDim.x) * kBlock) {
-        const float v = in[i];
-        mn = fminf(mn, v);
-        mx = fmaxf(mx, v);
+    const int64_t stride = int64_t(gridDim.x) * kBlock;
+    const int64_t t0 = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(in) & 15u) == 0) {   // 16-B loads, then the tail
+        const float4* in4 = reinterpret_cast<const float4*>(in);
+        const int64_t n4 = n / 4;
+        for (int64_t i = t0; i < n4; i += stride) {
+            const float4 v = in4[i];
+            mn = fminf(fminf(mn, v.x), fminf(v.y, fminf(v.z, v.w)));
+            mx = fmaxf(fmaxf(mx, v.x), fmaxf(v.y, fmaxf(v.z, v.w)));
+        }
+        for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
+            mn = fminf(mn, in[i]);
+            mx = fmaxf(mx, in[i]);
+        }
+    } else {
+        for (int64_t i = t0; i < n; i += stride) {
+            const float v = in[i];
+            mn = fminf(mn, v);
+            mx = fmaxf(mx, v);
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         mn = fminf(mn, __shfl_xor(mn, off, 64));
@@ -399,8 +709,6 @@ __device__ __forceinline__ int special_point(const float* __restrict__ dog, Dims
     return 0;
 }
 
-constexpr int kItems = 16;  // voxels per thread per chunk; chunk = kBlock * kItems
-
 // (x, y, z) of flat index i: 32-bit divisions when the volume allows (a 64-bit
 // division is a ~100-instruction software routine on the GPU)
 __device__ __forceinline__ void flat_coords(int64_t i, const Dims3& d, int64_t& x, int64_t& y, int64_t& z) {
@@ -417,108 +725,27 @@ __device__ __forceinline__ void flat_coords(int64_t i, const Dims3& d, int64_t& 
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_peaks_count(const float* __restrict__ dog, Dims3 d,
-                                                         float minv, int want_min, int want_max,
-                                                         int* __restrict__ counts) {
-    __shared__ int sh[kBlock / 64];
+// candidates of a DoG volume already in HBM (the fallback for Gaussians of 63 / 127 taps)
+__global__ __launch_bounds__(kBlock) void k_peaks_append(const float* __restrict__ dog, Dims3 d, PeakSink pk) {
     const int64_t n = d.nx * d.ny * d.nz;
-    const int64_t chunk0 = int64_t(blockIdx.x) * kBlock * kItems;
-    int cnt = 0;
-    for (int it = 0; it < kItems; ++it) {
-        const int64_t i = chunk0 + int64_t(it) * kBlock + threadIdx.x;
-        if (i >= n) break;
-        int64_t x, y, z;
-        flat_coords(i, d, x, y, z);
-        float v;
-        const int sp = special_point(dog, d, i, x, y, z, minv, v);
-        cnt += (sp == 2 && want_max) || (sp == 1 && want_min);
-    }
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int w = 0; w < kBlock / 64; ++w) t += sh[w];
-        counts[blockIdx.x] = t;
-    }
-}
-
-// exclusive scan of counts: one block of kScanThreads, each thread scans a contiguous
-// run of counts sequentially after a block-wide scan of the run totals
-constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void k_scan(const int* __restrict__ counts, int64_t nb,
-                                                       int64_t* __restrict__ offsets) {
-    __shared__ int64_t tot[kScanThreads];
-    const int t = threadIdx.x;
-    const int64_t per = (nb + kScanThreads - 1) / kScanThreads;
-    const int64_t b0 = min(nb, int64_t(t) * per), b1 = min(nb, b0 + per);
-    int64_t sum = 0;
-    for (int64_t b = b0; b < b1; ++b) sum += counts[b];
-    tot[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) {  // Hillis-Steele inclusive scan
-        const int64_t v = t >= off ? tot[t - off] : 0;
-        __syncthreads();
-        tot[t] += v;
-        __syncthreads();
-    }
-    int64_t run = tot[t] - sum;  // exclusive prefix of this run
-    for (int64_t b = b0; b < b1; ++b) {
-        offsets[b] = run;
-        run += counts[b];
-    }
-    if (t == kScanThreads - 1) offsets[nb] = tot[t];
-}
-
-struct PeakOut {
-    int32_t x, y, z;
-    float intensity;
-    int32_t is_min, is_max;
-};
-
-__global__ __launch_bounds__(kBlock) void k_peaks_write(const float* __restrict__ dog, Dims3 d,
-                                                         float minv, int want_min, int want_max,
-                                                         const int64_t* __restrict__ offsets,
-                                                         PeakOut* __restrict__ out, int64_t cap) {
-    __shared__ int wave_cnt[kBlock / 64];
-    __shared__ int64_t base_sh;
-    const int64_t n = d.nx * d.ny * d.nz;
-    const int64_t chunk0 = int64_t(blockIdx.x) * kBlock * kItems;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) base_sh = offsets[blockIdx.x];
-    __syncthreads();
-    for (int it = 0; it < kItems; ++it) {
-        const int64_t i = chunk0 + int64_t(it) * kBlock + threadIdx.x;
+    for (int64_t i0 = int64_t(blockIdx.x) * kBlock; i0 < n; i0 += int64_t(gridDim.x) * kBlock) {
+        const int64_t i = i0 + threadIdx.x;
         int sp = 0;
         float v = 0.0f;
         int64_t x = 0, y = 0, z = 0;
         if (i < n) {
             flat_coords(i, d, x, y, z);
-            sp = special_point(dog, d, i, x, y, z, minv, v);
+            sp = special_point(dog, d, i, x, y, z, pk.minv, v);
         }
-        const bool flag = (sp == 2 && want_max) || (sp == 1 && want_min);
-        const unsigned long long m = __ballot(flag);
-        if (lane == 0) wave_cnt[wid] = __popcll(m);
-        __syncthreads();
-        int prefix = 0;
-        for (int w = 0; w < wid; ++w) prefix += wave_cnt[w];
-        const int64_t pos = base_sh + prefix + __popcll(m & ((1ull << lane) - 1ull));
-        if (flag && pos < cap) {
-            PeakOut p;
-            p.x = int32_t(x); p.y = int32_t(y); p.z = int32_t(z);
-            p.intensity = fabsf(v);
-            p.is_min = sp == 1;
-            p.is_max = sp == 2;
-            out[pos] = p;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int t = 0;
-            for (int w = 0; w < kBlock / 64; ++w) t += wave_cnt[w];
-            base_sh += t;
-        }
-        __syncthreads();
+        const bool flag = (sp == 2 && pk.want_max) || (sp == 1 && pk.want_min);
+        sink_append(pk, flag, int(x), int(y), int(z), uint64_t(i), v, sp);
     }
+}
+
+__global__ void k_gather_peaks(const PeakOut* __restrict__ recs, const uint32_t* __restrict__ order, int64_t n,
+                               PeakOut* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = recs[order[i]];
 }
 
 unsigned grid_of(int64_t n, int64_t cap = 4096) {
@@ -756,24 +983,84 @@ __global__ void k_localize(const float* __restrict__ dog, Dims3 d, const PeakOut
     out[i] = o;
 }
 
-// the DoG image (kept on the device) and the reference-ordered peak list
-struct DogRun {
-    Dims3 d{};
-    DBuf<float> dog;
-    std::vector<PeakOut> peaks;
+// tuning knobs for A/B runs (tools/dog_bench.py); defaults are the measured best
+int dog_env(const char* name, int def) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : def;
+}
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable host memory: not registered with HIP
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice;
+}
+
+// Per-device DoG workspace, grown on demand and kept between calls (a 768^3 view needs
+// ~3.6 GB of G12 plus the candidate lists; hipMalloc / hipFree of that per call cost
+// more than the DoG itself).  One call at a time per device holds its mutex;
+// spim_dog_release_workspace frees it.
+struct DogWork {
+    std::mutex mu;
+    DBuf<float> in, dog, taps, mm, tmp_a, tmp_b, tmp_c, tmp_d;
+    DBuf<float2> g12;
+    DBuf<uint64_t> keys, keys_sorted;
+    DBuf<uint32_t> vals, vals_sorted;
+    DBuf<PeakOut> recs, peaks;
+    DBuf<unsigned> count;
+    DBuf<unsigned char> sort_tmp;
+    void release() {
+        for (DBuf<float>* b : {&in, &dog, &taps, &mm, &tmp_a, &tmp_b, &tmp_c, &tmp_d}) b->release();
+        g12.release();
+        keys.release(); keys_sorted.release(); vals.release(); vals_sorted.release();
+        recs.release(); peaks.release(); count.release(); sort_tmp.release();
+    }
 };
 
-void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
-             hipStream_t s, DogRun& r) {
+std::mutex g_dogwork_mu;
+std::map<int, std::unique_ptr<DogWork>> g_dogwork;
+
+DogWork& dog_work(int dev) {
+    std::lock_guard<std::mutex> lk(g_dogwork_mu);
+    auto& w = g_dogwork[dev];
+    if (!w) w.reset(new DogWork());
+    return *w;
+}
+
+template <typename T>
+void grow(DBuf<T>& b, size_t n) {
+    if (b.n < n) b.alloc(n);
+}
+
+// the DoG image (on the device) and the reference-ordered candidate list (on the device)
+struct DogRun {
+    Dims3 d{};
+    const float* dog = nullptr;   // nullptr when neither localisation nor the image was asked for
+    int64_t np = 0;
+    const PeakOut* dpeaks = nullptr;
+};
+
+int bits_for(uint64_t v) {
+    int b = 0;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b;
+}
+
+void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out, bool need_dog,
+             hipStream_t s, DogWork& w, DogRun& r) {
     SD_CHECK(img && dims && p, SPIMDECON_ERR_ARG, "null argument");
     SD_CHECK(dims[0] >= 1 && dims[1] >= 1 && dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
     SD_CHECK(p->localization == 0 || p->localization == 1, SPIMDECON_ERR_ARG,
              "localization must be 0 (none) or 1 (quadratic); the Gaussian fit is not implemented in "
              "the reference either (Localization.java:90-96)");
-    SD_CHECK(p->ij_threads >= 1, SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
+    SD_CHECK(p->ij_threads >= 1 && p->ij_threads < (1 << 20), SPIMDECON_ERR_ARG, "ij_threads must be >= 1");
     const Dims3 d{dims[0], dims[1], dims[2]};
     r.d = d;
     const int64_t n = d.nx * d.ny * d.nz;
+    SD_CHECK(n < (int64_t(1) << 40), SPIMDECON_ERR_ARG, "volume too large");
 
     // ProcessDOG.java:61-105
     const float min_peak = p->localization == 0 ? p->threshold : p->threshold / 10.0f;
@@ -798,62 +1085,127 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         kall.insert(kall.end(), k1[a].begin(), k1[a].end());
         kall.insert(kall.end(), k2[a].begin(), k2[a].end());
     }
-    DBuf<float> dk(kall.size());
-    SD_HIP(hipMemcpyAsync(dk.p, kall.data(), kall.size() * 4, hipMemcpyHostToDevice, s));
-    auto kp = [&](int axis, int which) { return dk.p + (2 * axis + which) * K; };
+    // the same taps interleaved per axis, (sigma1[j], sigma2[j]) pairs, for the fused kernels
+    for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < K; ++j) {
+            kall.push_back(k1[a][j]);
+            kall.push_back(k2[a][j]);
+        }
+    grow(w.taps, kall.size());
+    SD_HIP(hipMemcpyAsync(w.taps.p, kall.data(), kall.size() * 4, hipMemcpyHostToDevice, s));
+    auto kp = [&](int axis, int which) { return w.taps.p + (2 * axis + which) * K; };
+    auto kp2 = [&](int axis) { return reinterpret_cast<const float2*>(w.taps.p + 6 * K + 2 * axis * K); };
 
-    DBuf<float> b0(n), b1(n), b2(n), b3(n);
-    // img / dog_out may be host or device pointers (unified addressing infers the copy)
-    SD_HIP(hipMemcpyAsync(b0.p, img, n * 4, hipMemcpyDefault, s));
-    DBuf<float> mm(2 * 4096);
+    // the view: read in place when it already lives in HBM, else one upload
+    const float* in = img;
+    if (!is_device_ptr(img)) {
+        grow(w.in, size_t(n));
+        SD_HIP(hipMemcpyAsync(w.in.p, img, n * 4, hipMemcpyHostToDevice, s));
+        in = w.in.p;
+    }
+    grow(w.mm, 2 * 4096);
     const bool use_given = !(std::isnan(p->min_intensity) || std::isnan(p->max_intensity) ||
                              std::isinf(p->min_intensity) || std::isinf(p->max_intensity) ||
                              p->min_intensity == p->max_intensity);
     if (use_given) {
         const float h2[2] = {float(p->min_intensity), float(p->max_intensity)};
-        SD_HIP(hipMemcpyAsync(mm.p, h2, 8, hipMemcpyHostToDevice, s));
+        SD_HIP(hipMemcpyAsync(w.mm.p, h2, 8, hipMemcpyHostToDevice, s));
     } else {
         const unsigned nb = grid_of(n);
-        hipLaunchKernelGGL(k_minmax, dim3(nb), dim3(kBlock), 0, s, b0.p, n, mm.p);
-        hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, s, mm.p, int(nb));
+        hipLaunchKernelGGL(k_minmax, dim3(nb), dim3(kBlock), 0, s, in, n, w.mm.p);
+        hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, s, w.mm.p, int(nb));
         SD_HIP(hipGetLastError());
     }
-    // x-pass (normalise fused) -> b1 (sigma1), b2 (sigma2)
-    sep_pass(d, 0, b0.p, b0.p, kp(0, 0), kp(0, 1), K, OOB_MIRROR, 0.f, b1.p, b2.p, false, 0.f, mm.p, s);
-    // y-pass: b1 -> b3, b2 -> b0
-    sep_pass(d, 1, b1.p, b2.p, kp(1, 0), kp(1, 1), K, OOB_MIRROR, 0.f, b3.p, b0.p, false, 0.f, nullptr, s);
-    // z-pass + DoG: (b3, b0) -> b1 = (G2 - G1) * kinv
-    sep_pass(d, 2, b3.p, b0.p, kp(2, 0), kp(2, 1), K, OOB_MIRROR, 0.f, b1.p, nullptr, true, kinv,
-             nullptr, s);
-    const float* dog = b1.p;
-    if (dog_out) SD_HIP(hipMemcpyAsync(dog_out, dog, n * 4, hipMemcpyDefault, s));
-
-    // peaks: order-preserving compaction in flat order
-    const int64_t chunk = int64_t(kBlock) * kItems;
-    const int64_t nb = ceil_div(n, chunk);
-    DBuf<int> counts(nb);
-    DBuf<int64_t> offsets(nb + 1);
-    const int wmin = p->find_min ? 1 : 0, wmax = p->find_max ? 1 : 0;
-    hipLaunchKernelGGL(k_peaks_count, dim3(unsigned(nb)), dim3(kBlock), 0, s, dog, d, min_peak, wmin,
-                       wmax, counts.p);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, counts.p, nb, offsets.p);
-    SD_HIP(hipGetLastError());
-    int64_t total = 0;
-    SD_HIP(hipMemcpyAsync(&total, offsets.p + nb, 8, hipMemcpyDeviceToHost, s));
-    SD_HIP(hipStreamSynchronize(s));
-    DBuf<PeakOut> dpk(std::max<int64_t>(total, 1));
-    hipLaunchKernelGGL(k_peaks_write, dim3(unsigned(nb)), dim3(kBlock), 0, s, dog, d, min_peak, wmin,
-                       wmax, offsets.p, dpk.p, total);
-    SD_HIP(hipGetLastError());
-    r.peaks.resize(total);
-    if (total)
-        SD_HIP(hipMemcpyAsync(r.peaks.data(), dpk.p, total * sizeof(PeakOut), hipMemcpyDeviceToHost, s));
-    SD_HIP(hipStreamSynchronize(s));
-    // reference order: per-thread lists by x % T, each in flat order (InteractiveIntegral.java:394,437-438)
+    // DoG destination: the caller's device buffer, else the workspace (copied out at the end)
+    float* dogp = nullptr;
+    const bool dog_dev = dog_out && is_device_ptr(dog_out);
+    if (need_dog) {
+        if (dog_dev) {
+            dogp = dog_out;
+        } else {
+            grow(w.dog, size_t(n));
+            dogp = w.dog.p;
+        }
+    }
+    grow(w.count, 1);
+    unsigned cap = unsigned(std::min<int64_t>(std::max<int64_t>(int64_t(1) << 16, n / 256), int64_t(1) << 30));
+    cap = std::max<unsigned>(cap, unsigned(std::min<size_t>(w.recs.n, size_t(1) << 30)));
     const int T = p->ij_threads;
-    std::stable_sort(r.peaks.begin(), r.peaks.end(),
-                     [T](const PeakOut& a, const PeakOut& b) { return (a.x % T) < (b.x % T); });
-    r.dog = std::move(b1);
+    const int wmin = p->find_min ? 1 : 0, wmax = p->find_max ? 1 : 0;
+    const bool fused = (K == 7 || K == 15 || K == 31) && n < (int64_t(1) << 32) && d.ny <= 65535 * 32 &&
+                       d.nz <= 65535;
+    const int zc = std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk));
+    const int ty = dog_env("SPIMDECON_DOG_XY_TY", 48) == 32 ? 32 : 48;
+    const int by = dog_env("SPIMDECON_DOG_Z_BY", 8) == 16 ? 16 : 8;
+    const dim3 gxy(unsigned(ceil_div(d.nx, kDxyTX)), unsigned(ceil_div(d.ny, ty)), unsigned(d.nz));
+    const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, kDzBX - 2))),
+                  unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, by - 2))), unsigned(ceil_div(d.nz, zc)));
+    bool store_dog = need_dog;
+    if (fused) {
+        grow(w.g12, size_t(n));
+#define SD_DOGXY(KV)                                                                                        \
+        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p);
+        if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
+#undef SD_DOGXY
+        SD_HIP(hipGetLastError());
+    } else {
+        // Gaussians of 63 / 127 taps: the separate passes, then a candidate pass over the DoG
+        grow(w.tmp_a, size_t(n));
+        grow(w.tmp_b, size_t(n));
+        grow(w.tmp_c, size_t(n));
+        grow(w.tmp_d, size_t(n));
+        if (!dogp) {
+            grow(w.dog, size_t(n));
+            dogp = w.dog.p;
+        }
+        sep_pass(d, 0, in, in, kp(0, 0), kp(0, 1), K, OOB_MIRROR, 0.f, w.tmp_a.p, w.tmp_b.p, false, 0.f, w.mm.p, s);
+        sep_pass(d, 1, w.tmp_a.p, w.tmp_b.p, kp(1, 0), kp(1, 1), K, OOB_MIRROR, 0.f, w.tmp_c.p, w.tmp_d.p, false,
+                 0.f, nullptr, s);
+        sep_pass(d, 2, w.tmp_c.p, w.tmp_d.p, kp(2, 0), kp(2, 1), K, OOB_MIRROR, 0.f, dogp, nullptr, true, kinv,
+                 nullptr, s);
+    }
+    unsigned total = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        grow(w.keys, cap);
+        grow(w.vals, cap);
+        grow(w.recs, cap);
+        SD_HIP(hipMemsetAsync(w.count.p, 0, sizeof(unsigned), s));
+        const PeakSink pk{min_peak, wmin, wmax, T, w.keys.p, w.vals.p, w.recs.p, w.count.p, cap};
+        if (fused) {
+            float* dst = store_dog ? dogp : nullptr;
+#define SD_DOGZ(KV)                                                                                          \
+            if (by == 8) hipLaunchKernelGGL((k_dog_z<KV, 8>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk); \
+            else hipLaunchKernelGGL((k_dog_z<KV, 16>), gz, dim3(kDzBX * 16), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk);
+            if (K == 7) { SD_DOGZ(7) } else if (K == 15) { SD_DOGZ(15) } else { SD_DOGZ(31) }
+#undef SD_DOGZ
+        } else {
+            hipLaunchKernelGGL(k_peaks_append, dim3(grid_of(n)), dim3(kBlock), 0, s, dogp, d, pk);
+        }
+        SD_HIP(hipGetLastError());
+        SD_HIP(hipMemcpyAsync(&total, w.count.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        SD_HIP(hipStreamSynchronize(s));
+        if (total <= cap) break;
+        cap = total;          // rerun with room for every candidate (the DoG is already stored)
+        store_dog = false;
+    }
+    // reference order: ascending (x % T) << 40 | flat
+    r.np = total;
+    r.dog = dogp;
+    if (total > 0) {
+        grow(w.keys_sorted, total);
+        grow(w.vals_sorted, total);
+        grow(w.peaks, total);
+        const int end_bit = 40 + bits_for(uint64_t(T - 1));
+        const size_t tb = peak_sort_temp_bytes(total, end_bit);
+        grow(w.sort_tmp, std::max<size_t>(tb, 1));
+        peak_sort(w.sort_tmp.p, tb, w.keys.p, w.keys_sorted.p, w.vals.p, w.vals_sorted.p, total, end_bit, s);
+        hipLaunchKernelGGL(k_gather_peaks, dim3(unsigned(ceil_div(total, 256))), dim3(256), 0, s, w.recs.p,
+                           w.vals_sorted.p, int64_t(total), w.peaks.p);
+        SD_HIP(hipGetLastError());
+        r.dpeaks = w.peaks.p;
+    }
+    if (dog_out && !dog_dev) SD_HIP(hipMemcpyAsync(dog_out, dogp, n * 4, hipMemcpyDeviceToHost, s));
 }
 
 struct StreamHolder {
@@ -869,21 +1221,23 @@ void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p
     SD_CHECK(npeaks && p, SPIMDECON_ERR_ARG, "null argument");
     check_device(p->device);
     DeviceGuard guard(p->device);
+    DogWork& w = dog_work(p->device);
+    std::lock_guard<std::mutex> lk(w.mu);
     StreamHolder sh;
     DogRun r;
-    dog_run(img, dims, p, dog_out, sh.s, r);
-    const int64_t total = int64_t(r.peaks.size());
-    *npeaks = total;
-    if (peaks) {
-        const int64_t m = std::min(total, max_peaks);
-        for (int64_t i = 0; i < m; ++i) {
-            peaks[i].x = r.peaks[i].x;
-            peaks[i].y = r.peaks[i].y;
-            peaks[i].z = r.peaks[i].z;
-            peaks[i].intensity = r.peaks[i].intensity;
-            peaks[i].is_min = r.peaks[i].is_min;
-            peaks[i].is_max = r.peaks[i].is_max;
-        }
+    dog_run(img, dims, p, dog_out, dog_out != nullptr, sh.s, w, r);
+    *npeaks = r.np;
+    const int64_t m = peaks ? std::min(r.np, max_peaks) : 0;
+    std::vector<PeakOut> hp(std::max<int64_t>(m, 0));
+    if (m > 0) SD_HIP(hipMemcpyAsync(hp.data(), r.dpeaks, m * sizeof(PeakOut), hipMemcpyDeviceToHost, sh.s));
+    SD_HIP(hipStreamSynchronize(sh.s));
+    for (int64_t i = 0; i < m; ++i) {
+        peaks[i].x = hp[i].x;
+        peaks[i].y = hp[i].y;
+        peaks[i].z = hp[i].z;
+        peaks[i].intensity = hp[i].intensity;
+        peaks[i].is_min = hp[i].is_min;
+        peaks[i].is_max = hp[i].is_max;
     }
 }
 
@@ -893,26 +1247,29 @@ void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_p
     SD_CHECK(nout && p, SPIMDECON_ERR_ARG, "null argument");
     check_device(p->device);
     DeviceGuard guard(p->device);
+    DogWork& w = dog_work(p->device);
+    std::lock_guard<std::mutex> lk(w.mu);
     StreamHolder sh;
     DogRun r;
-    dog_run(img, dims, p, dog_out, sh.s, r);
+    dog_run(img, dims, p, dog_out, p->localization == 1 || dog_out != nullptr, sh.s, w, r);
+    const int64_t np = r.np;
+    std::vector<PeakOut> hp(np);
+    if (np > 0) SD_HIP(hipMemcpyAsync(hp.data(), r.dpeaks, np * sizeof(PeakOut), hipMemcpyDeviceToHost, sh.s));
     std::vector<spim_interest_point> pts;
-    const int64_t np = int64_t(r.peaks.size());
     if (p->localization == 0) {  // Localization.noLocalization (:19-45)
+        SD_HIP(hipStreamSynchronize(sh.s));
         pts.resize(np);
         for (int64_t i = 0; i < np; ++i) {
-            pts[i].pos[0] = r.peaks[i].x;
-            pts[i].pos[1] = r.peaks[i].y;
-            pts[i].pos[2] = r.peaks[i].z;
-            pts[i].intensity = r.peaks[i].intensity;
-            pts[i].is_max = r.peaks[i].is_max;
+            pts[i].pos[0] = hp[i].x;
+            pts[i].pos[1] = hp[i].y;
+            pts[i].pos[2] = hp[i].z;
+            pts[i].intensity = hp[i].intensity;
+            pts[i].is_max = hp[i].is_max;
         }
     } else if (np > 0) {  // Localization.computeQuadraticLocalization (:47-88)
-        DBuf<PeakOut> dpk(np);
         DBuf<LocOut> dloc(np);
-        SD_HIP(hipMemcpyAsync(dpk.p, r.peaks.data(), np * sizeof(PeakOut), hipMemcpyHostToDevice, sh.s));
-        hipLaunchKernelGGL(k_localize, dim3(unsigned(ceil_div(np, 256))), dim3(256), 0, sh.s, r.dog.p, r.d,
-                           dpk.p, np, dloc.p);
+        hipLaunchKernelGGL(k_localize, dim3(unsigned(ceil_div(np, 256))), dim3(256), 0, sh.s, r.dog, r.d,
+                           r.dpeaks, np, dloc.p);
         SD_HIP(hipGetLastError());
         std::vector<LocOut> loc(np);
         SD_HIP(hipMemcpyAsync(loc.data(), dloc.p, np * sizeof(LocOut), hipMemcpyDeviceToHost, sh.s));
@@ -922,12 +1279,23 @@ void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_p
             spim_interest_point ip{};
             for (int a = 0; a < 3; ++a) ip.pos[a] = loc[i].pos[a];
             ip.intensity = loc[i].value;
-            ip.is_max = r.peaks[i].is_max;
+            ip.is_max = hp[i].is_max;
             pts.push_back(ip);
         }
+    } else {
+        SD_HIP(hipStreamSynchronize(sh.s));
     }
     *nout = int64_t(pts.size());
     if (out) std::copy(pts.begin(), pts.begin() + std::min<int64_t>(max_out, int64_t(pts.size())), out);
+}
+
+void dog_release_workspace(int dev) {
+    check_device(dev);
+    DeviceGuard guard(dev);
+    DogWork& w = dog_work(dev);
+    std::lock_guard<std::mutex> lk(w.mu);
+    SD_HIP(hipDeviceSynchronize());
+    w.release();
 }
 
 }  // namespace spimdecon
@@ -973,6 +1341,10 @@ extern "C" int spim_dog_interest_points(const float* img, const int64_t* dims, c
                                         float* dog_out, spim_interest_point* out, int64_t max_out,
                                         int64_t* nout) {
     return guarded([&] { dog_interest_points(img, dims, p, dog_out, out, max_out, nout); });
+}
+
+extern "C" int spim_dog_release_workspace(int device) {
+    return guarded([&] { dog_release_workspace(device); });
 }
 
 extern "C" int spim_dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p,

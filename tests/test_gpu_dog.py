@@ -106,3 +106,79 @@ def test_dog_device_resident_input(gpu):
     np.testing.assert_array_equal(ddog.cpu().numpy(), d)
     for i, q in enumerate(pts):
         assert tuple(out[i].pos) == tuple(q.location)
+
+
+# ---------------------------------------------------------------- fused DoG path (k_dog_xy / k_dog_z)
+
+@pytest.mark.parametrize("sigma,taps", [(1.0, 7), (1.8, 15), (4.0, 31), (8.0, 63)])
+def test_dog_tap_sizes_tiles_and_chunks(gpu, sigma, taps):
+    """Every Gaussian size class: 7 / 15 / 31 taps on the fused kernels, 63 on the
+    separate passes + candidate pass.  150 planes = 3 z chunks of 64 (the last one
+    ragged); 70 rows = several 16-row boxes and 32-row xy tiles; 131 columns = three
+    64-column boxes with their 1-voxel halo rings.  Bit-identical DoG and peak list."""
+    s1, s2, _, _ = dog_ref.dog_sigmas(sigma, (0.5, 0.5, 0.5))
+    assert len(dog_ref.cuda_kernels(s1)[0]) == taps or len(dog_ref.cuda_kernels(s2)[0]) == taps
+    img = bead_stack(shape=(150, 70, 131), cid=21)
+    pts, d = dog.compute(img, sigma=sigma, threshold=0.002, find_min=True, find_max=True, return_dog=True,
+                         keep_intensity=True)
+    exp, dref = dog_ref.process_dog(img, sigma, 0.002, find_min=True, find_max=True)
+    np.testing.assert_array_equal(d, dref)
+    assert len(exp) > 5
+    assert [tuple(int(c) for c in p.location) for p in pts] == [e[:3] for e in exp]
+    np.testing.assert_array_equal([p.intensity for p in pts], np.float32([e[3] for e in exp]))
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (1, 5, 7), (3, 3, 3), (2, 9, 4), (5, 1, 70), (70, 3, 65),
+                                   (4, 17, 3), (66, 18, 66)])
+def test_dog_small_and_thin_volumes(gpu, shape):
+    """Volumes thinner than the kernel, the boxes or the peak border (mirror indices
+    folding several times); threshold 0 on noise: every extremum is a candidate."""
+    rng = np.random.default_rng(sum(shape))
+    img = rng.random(shape, dtype=np.float32)
+    pts, d = dog.compute(img, threshold=0.0, find_min=True, find_max=True, return_dog=True,
+                         keep_intensity=True, ij_threads=3)
+    exp, dref = dog_ref.process_dog(img, 1.8, 0.0, find_min=True, find_max=True, ij_threads=3)
+    np.testing.assert_array_equal(d, dref)
+    assert [tuple(int(c) for c in p.location) for p in pts] == [e[:3] for e in exp]
+
+
+def test_dog_plateau_overflows_candidate_capacity(gpu):
+    """A constant volume at threshold 0: every interior voxel is a (plateau) extremum
+    (238,328 > the 65,536 initial candidate capacity): the library reruns the peak
+    kernel with room for all and keeps the reference order."""
+    img = np.full((64, 64, 64), 3.0, np.float32)
+    pk = dog.simple_peaks(img, threshold=0.0, find_min=True, find_max=True)
+    _, dref = dog_ref.process_dog(img, 1.8, 0.0)
+    exp = dog_ref.find_peaks(dref, 0.0)
+    assert len(pk) == len(exp) == 62 ** 3
+    assert [q[:3] for q in pk] == [e[:3] for e in exp]
+    assert [(q[4], q[5]) for q in pk] == [(e[4], e[5]) for e in exp]
+
+
+def test_dog_nan_planes_take_the_comparison_loop(gpu):
+    """NaN in the image spreads into the DoG; a NaN neighbour fails every comparison
+    in the reference (isSpecialPoint), which the min/max box test would not see --
+    the planes holding NaN are tested by the comparison loop.  Checked against the
+    oracle's peak finder on the library's own DoG image (the oracle's convolution
+    skips zero taps, so its NaN footprint differs for padded kernels)."""
+    img = bead_stack(shape=(40, 44, 48), cid=22)
+    img[20, 22, 24] = np.nan
+    img[5, 40, 3] = np.nan
+    pk = dog.simple_peaks(img, threshold=0.001, find_min=True, find_max=True, min_intensity=0.0,
+                          max_intensity=4000.0)
+    _, d = dog.compute(img, threshold=0.001, min_intensity=0.0, max_intensity=4000.0, return_dog=True)
+    assert np.isnan(d).sum() > 1000
+    exp = dog_ref.find_peaks(d, 0.001)
+    assert [q[:3] for q in pk] == [e[:3] for e in exp] and len(exp) > 10
+    assert [(q[4], q[5]) for q in pk] == [(e[4], e[5]) for e in exp]
+
+
+def test_dog_workspace_release_and_reuse(gpu):
+    """The per-device workspace grows to the largest view and is reused; releasing it
+    and calling again gives the same result."""
+    from spim_registration_amd import _lib
+    img = bead_stack(shape=(24, 26, 30), cid=23)
+    a = dog.compute(img, localization=1, keep_intensity=True)
+    _lib.check(_lib.load().spim_dog_release_workspace(0))
+    b = dog.compute(img, localization=1, keep_intensity=True)
+    assert [(p.location, p.intensity) for p in a] == [(p.location, p.intensity) for p in b]

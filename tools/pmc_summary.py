@@ -38,6 +38,8 @@ def main(out, json_out=None, dims=None, fp16=False):
     cols = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
             "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS",
             "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"]
+    cols += [c for c in ("SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU")
+             if any(c in v for v in vals.values())]
     print("| kernel | us (avg) | HBM MB/launch (2*FETCH+WRITE) | GB/s | " + " | ".join(cols) + " |")
     print("|---|" + "---|" * (3 + len(cols)))
     table = {}
