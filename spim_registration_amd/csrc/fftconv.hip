@@ -961,7 +961,59 @@ int engine_zpass_mode(const SpectralPlan& p, bool compact) {
     return engine_zdirect_ok(p) ? 2 : 1;
 }
 
+// k_zdma (LDS-DMA, double-buffered) when both buffers fit; SPIMDECON_ZDMA=0 keeps k_zdirect
+static bool zdma_enabled() {
+    const char* e = std::getenv("SPIMDECON_ZDMA");
+    return !(e && e[0] == '0');
+}
+
+// outputs per thread round: the fewest FMA + window-read slots over the rounds nz needs
+static int zdma_opt(int nz, int KC) {
+    int best = 1;
+    int64_t bc = -1;
+    for (int opt : {1, 5, 17}) {
+        const int64_t c = int64_t(zdma_rounds(nz, opt)) * (2 * (2 * KC + 1) * opt + 2 * (opt + 2 * KC));
+        if (bc < 0 || c < bc) {
+            bc = c;
+            best = opt;
+        }
+    }
+    return best;
+}
+
+static size_t zdma_lds(const SpectralPlan& p, int KC, int opt) {
+    return size_t(2) * size_t(zdma_slots(int(p.g.Mz), int(p.g.nz), KC, opt) + zdma_tap_slots(KC)) * kZdTX *
+           sizeof(float2);
+}
+
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
+    if (engine_zdirect_ok(p) && zdma_enabled()) {
+        const int KC = zdirect_kc_bound(p.g.cz);
+        const int opt = zdma_opt(int(p.g.nz), KC);
+        const size_t lds = zdma_lds(p, KC, opt);
+        if (lds <= 160 * 1024) {
+            const int64_t ntiles = (p.Hp / kZdTX) * p.g.My;
+            const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+            const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu));
+            const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
+            const float kscale = float(p.g.Mz);
+            bool done = false;
+#define SD_ZM(KCV, OPTV)                                                                               \
+            if (!done && KC == (KCV) && opt == (OPTV)) {                                               \
+                SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdma<KCV, OPTV>),          \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));     \
+                hipLaunchKernelGGL((k_zdma<KCV, OPTV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, \
+                                   Kc, p.g.cz, bytes, kscale);                                         \
+                done = true;                                                                           \
+            }
+            SD_ZM(4, 1) SD_ZM(4, 5) SD_ZM(4, 17) SD_ZM(8, 1) SD_ZM(8, 5) SD_ZM(8, 17)
+            SD_ZM(12, 1) SD_ZM(12, 5) SD_ZM(12, 17)
+#undef SD_ZM
+            SD_CHECK(done, SPIMDECON_ERR_ARG, "no LDS-DMA z kernel for this kernel size");
+            SD_HIP(hipGetLastError());
+            return;
+        }
+    }
     if (engine_zdirect_ok(p)) {
         const int KC = zdirect_kc_bound(p.g.cz);
         const size_t lds = zdirect_lds(p, KC);
