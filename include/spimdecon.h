@@ -220,7 +220,8 @@ int mvd_run(mvd_session* h, int iters, double lambda, double* stats);
 /* final mask: psi = 0 where no view has data (MVDeconvolution.java:180-187) */
 int mvd_apply_mask(mvd_session* h);
 
-/* copy this rank's psi to host (dims of params) */
+/* copy this rank's psi to out (dims of params); out may be a host or a device
+ * pointer (unified addressing: a device-resident result skips the host) */
 int mvd_get_psi(mvd_session* h, float* out);
 /* device pointer of local slab s's psi (valid until mvd_destroy); x-fastest
  * [z][y][x] of the slab, or [y][z][x] when the session splits along y */

@@ -699,20 +699,23 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // modes: planes stored) -- the RL loop only reads the nz interior planes back
     if (nout < 0) nout = int(p.g.Mz);
     const int L = f.L;
-    // 16-column tiles (128-B row segments); 8 columns when a 16-column tile of the
-    // length would not fit the LDS (L > 1204, e.g. 2100 for 2048-wide volumes).
-    // 8-column tiles measured slower for the fused z pass (0.69 vs 0.60 ms)
-    const int TX = size_t(L * k2fTX + L) * sizeof(float2) <= 160 * 1024 ? k2fTX : 8;
+    // 16-column tiles (128-B row segments) when they fit the LDS budget of the factor
+    // pair's occupancy (80 KB at 32 threads per column, 160 KB at 64); else 8 columns
+    // (8-column tiles measured slower for the fused z pass, 0.69 vs 0.60 ms, but beat
+    // the Stockham passes: L = 640 / 800 / 1024 at 32 threads, 2100 at 64)
+    const int tr = (f.n1 > 32 || f.n2 > 32) ? 64 : 32;  // SD_2F_TR
+    const size_t budget = size_t(tr == 64 ? 160 : 80) * 1024;
+    auto tile_lds = [&](int tx) { return size_t(L * tx + L + (MODE == 5 ? f.n2 * tx : 0)) * sizeof(float2); };
+    const int TX = tile_lds(k2fTX) <= budget ? k2fTX : 8;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
-    const size_t lds = size_t(L * TX + L + (MODE == 5 ? f.n2 * TX : 0)) * sizeof(float2);
+    const size_t lds = tile_lds(TX);
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);
     const uint64_t kbytes = MODE == 5 ? uint64_t(kplanes) * p.Hp * p.g.My * sizeof(float2)
                                       : (MODE >= 2 ? bytes : 0);
-    const int tr = (f.n1 > 32 || f.n2 > 32) ? 64 : 32;  // SD_2F_TR
     // the fused z modes hold two length-N2 vectors per thread: TR = 64 (N2 > 32) would
     // spill, so long lengths run them on the Stockham column pass
     if (MODE >= 2 && tr == 64) return false;
-    if (lds > (tr == 64 ? 160 : 80) * 1024 || (AXIS == 2 && bytes >= (uint64_t(1) << 31))) return false;
+    if (lds > budget || (AXIS == 2 && bytes >= (uint64_t(1) << 31))) return false;
     if (MODE == 5 && (AXIS != 2 || kplanes > f.n2)) return false;
     // AXIS 1 resources span one z plane from the tile's first column
     const uint32_t rbytes = AXIS == 1 ? uint32_t(uint64_t(p.g.My * p.Hp) * sizeof(float2)) : uint32_t(bytes);
@@ -736,7 +739,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
         }                                                                                                  \
     }
 #define SD_2F_C(A, B) \
-    SD_2F_C1(A, B, 16) if constexpr ((A) * (B) > 1204) { SD_2F_C1(A, B, 8) }
+    SD_2F_C1(A, B, 16) if constexpr ((A) * (B) > 600) { SD_2F_C1(A, B, 8) }
     SD_2F_SIZES(SD_2F_C)
 #undef SD_2F_C
 #undef SD_2F_C1
@@ -884,7 +887,7 @@ void engine_kernel_spectrum(const SpectralPlan& p, const float* d_kernel, int kx
 bool engine_kernel_compact_ok(const SpectralPlan& p) {
     const int kc = p.g.cz;
     return p.fz.n1 && p.fz.n1 <= 32 && p.fz.n2 <= 32 && 2 * kc + 1 <= p.fz.n2 &&  // MODE 5 is TR = 32 only
-           size_t(p.fz.L * k2fTX + p.fz.L + p.fz.n2 * k2fTX) * sizeof(float2) <= 80 * 1024 &&
+           size_t(p.fz.L * 8 + p.fz.L + p.fz.n2 * 8) * sizeof(float2) <= 80 * 1024 &&   // 8- or 16-column tiles
            uint64_t(p.spectrum_elems()) * sizeof(float2) < (uint64_t(1) << 31);
 }
 
@@ -933,8 +936,47 @@ static bool zdirect_enabled() {
 // kc 12 (25 taps) 0.298 ms with 4 outputs per round (0.437 with 8: the taps and
 // accumulators spilled).  Larger kernels keep the FFT z pass.
 static int zdirect_kc_bound(int kc) {
-    for (int b : {4, 8, 12})
+    for (int b : {4, 8, 12, 16})
         if (kc <= b) return b;
+    return 0;
+}
+
+// k_zdma (LDS-DMA, double-buffered) when both buffers fit; SPIMDECON_ZDMA=0 keeps k_zdirect
+static bool zdma_enabled() {
+    const char* e = std::getenv("SPIMDECON_ZDMA");
+    return !(e && e[0] == '0');
+}
+
+// outputs per thread round: the fewest FMA + window-read slots over the rounds nz needs
+static int zdma_opt(int nz, int KC, int tx) {
+    int best = 1;
+    int64_t bc = -1;
+    // (33 taps: 17 outputs per round would spill the taps and accumulators)
+    for (int opt : {1, 5, KC > 12 ? 9 : 17}) {
+        const int rounds = tx == 16 ? zdma_rounds(nz, opt, 16) : zdma_rounds(nz, opt, 8);
+        const int64_t c = int64_t(rounds) * (2 * (2 * KC + 1) * opt + 2 * (opt + 2 * KC));
+        if (bc < 0 || c < bc) {
+            bc = c;
+            best = opt;
+        }
+    }
+    return best;
+}
+
+static size_t zdma_lds(int64_t Mz, int64_t nz, int KC, int opt, int tx) {
+    const int slots = tx == 16 ? zdma_slots(int(Mz), int(nz), KC, opt, 16) + zdma_tap_slots(KC, 16)
+                               : zdma_slots(int(Mz), int(nz), KC, opt, 8) + zdma_tap_slots(KC, 8);
+    return size_t(2) * size_t(slots) * size_t(tx) * sizeof(float2);
+}
+
+// tile width of the LDS-DMA kernel for this geometry: 16 columns when both buffers
+// fit, else 8; 0 = it does not apply (33-tap kernels run only there)
+static int zdma_tx(int64_t Mz, int cz) {
+    const int KC = zdirect_kc_bound(cz);
+    const int64_t nz = Mz - 2 * cz;
+    if (!zdma_enabled() || KC == 0 || nz < 1) return 0;
+    for (int tx : {16, 8})
+        if (zdma_lds(Mz, nz, KC, zdma_opt(int(nz), KC, tx), tx) <= 160 * 1024) return tx;
     return 0;
 }
 
@@ -949,7 +991,7 @@ bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
     // Mz >= KC: the wrap copies of k_zdirect fill every window slot only then (a
     // window slot left unwritten would multiply stale LDS by a zero tap: 0 * NaN)
     return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC && lds <= 160 * 1024 &&
-           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
+           (KC <= 12 || zdma_tx(Mz, cz) > 0) && uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
 }
 
 bool engine_zdirect_ok(const SpectralPlan& p) {
@@ -961,58 +1003,34 @@ int engine_zpass_mode(const SpectralPlan& p, bool compact) {
     return engine_zdirect_ok(p) ? 2 : 1;
 }
 
-// k_zdma (LDS-DMA, double-buffered) when both buffers fit; SPIMDECON_ZDMA=0 keeps k_zdirect
-static bool zdma_enabled() {
-    const char* e = std::getenv("SPIMDECON_ZDMA");
-    return !(e && e[0] == '0');
-}
-
-// outputs per thread round: the fewest FMA + window-read slots over the rounds nz needs
-static int zdma_opt(int nz, int KC) {
-    int best = 1;
-    int64_t bc = -1;
-    for (int opt : {1, 5, 17}) {
-        const int64_t c = int64_t(zdma_rounds(nz, opt)) * (2 * (2 * KC + 1) * opt + 2 * (opt + 2 * KC));
-        if (bc < 0 || c < bc) {
-            bc = c;
-            best = opt;
-        }
-    }
-    return best;
-}
-
-static size_t zdma_lds(const SpectralPlan& p, int KC, int opt) {
-    return size_t(2) * size_t(zdma_slots(int(p.g.Mz), int(p.g.nz), KC, opt) + zdma_tap_slots(KC)) * kZdTX *
-           sizeof(float2);
-}
-
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
-    if (engine_zdirect_ok(p) && zdma_enabled()) {
+    if (engine_zdirect_ok(p) && zdma_tx(p.g.Mz, p.g.cz) > 0 && p.Hp % 16 == 0) {
         const int KC = zdirect_kc_bound(p.g.cz);
-        const int opt = zdma_opt(int(p.g.nz), KC);
-        const size_t lds = zdma_lds(p, KC, opt);
-        if (lds <= 160 * 1024) {
-            const int64_t ntiles = (p.Hp / kZdTX) * p.g.My;
-            const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-            const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu));
-            const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
-            const float kscale = float(p.g.Mz);
-            bool done = false;
-#define SD_ZM(KCV, OPTV)                                                                               \
-            if (!done && KC == (KCV) && opt == (OPTV)) {                                               \
-                SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdma<KCV, OPTV>),          \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));     \
-                hipLaunchKernelGGL((k_zdma<KCV, OPTV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, \
-                                   Kc, p.g.cz, bytes, kscale);                                         \
-                done = true;                                                                           \
-            }
-            SD_ZM(4, 1) SD_ZM(4, 5) SD_ZM(4, 17) SD_ZM(8, 1) SD_ZM(8, 5) SD_ZM(8, 17)
-            SD_ZM(12, 1) SD_ZM(12, 5) SD_ZM(12, 17)
-#undef SD_ZM
-            SD_CHECK(done, SPIMDECON_ERR_ARG, "no LDS-DMA z kernel for this kernel size");
-            SD_HIP(hipGetLastError());
-            return;
+        const int tx = zdma_tx(p.g.Mz, p.g.cz);
+        const int opt = zdma_opt(int(p.g.nz), KC, tx);
+        const size_t lds = zdma_lds(p.g.Mz, p.g.nz, KC, opt, tx);
+        const int64_t ntiles = (p.Hp / tx) * p.g.My;
+        const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
+        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu));
+        const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
+        const float kscale = float(p.g.Mz);
+        bool done = false;
+#define SD_ZM(KCV, OPTV, TXV)                                                                          \
+        if (!done && KC == (KCV) && opt == (OPTV) && tx == (TXV)) {                                    \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdma<KCV, OPTV, TXV>),         \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));         \
+            hipLaunchKernelGGL((k_zdma<KCV, OPTV, TXV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, \
+                               Kc, p.g.cz, bytes, kscale);                                             \
+            done = true;                                                                               \
         }
+#define SD_ZM2(KCV, OPTV) SD_ZM(KCV, OPTV, 16) SD_ZM(KCV, OPTV, 8)
+        SD_ZM2(4, 1) SD_ZM2(4, 5) SD_ZM2(4, 17) SD_ZM2(8, 1) SD_ZM2(8, 5) SD_ZM2(8, 17)
+        SD_ZM2(12, 1) SD_ZM2(12, 5) SD_ZM2(12, 17) SD_ZM2(16, 1) SD_ZM2(16, 5) SD_ZM2(16, 9)
+#undef SD_ZM2
+#undef SD_ZM
+        SD_CHECK(done, SPIMDECON_ERR_ARG, "no LDS-DMA z kernel for this kernel size");
+        SD_HIP(hipGetLastError());
+        return;
     }
     if (engine_zdirect_ok(p)) {
         const int KC = zdirect_kc_bound(p.g.cz);

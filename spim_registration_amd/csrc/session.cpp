@@ -192,14 +192,14 @@ void Session::load_slab(const float* src, hipMemcpyKind kind, const SlabState& s
 void Session::store_slab(const SlabState& sl, const float* src, float* out, DBuf<float>& tmp, hipStream_t st) const {
     const int64_t nx = odims_[0], ny = odims_[1], nz = odims_[2];
     if (axis_ == 0) {
-        SD_HIP(hipMemcpyAsync(out + sl.local_z0 * nx * ny, src, size_t(sl.n) * 4, hipMemcpyDeviceToHost, st));
+        SD_HIP(hipMemcpyAsync(out + sl.local_z0 * nx * ny, src, size_t(sl.n) * 4, hipMemcpyDefault, st));
         return;
     }
     const int64_t y0 = sl.local_z0, ys = sl.g.nz;
     if (tmp.n < size_t(sl.n)) tmp.alloc(sl.n);
     launch_swap_outer(src, tmp.p, nx, nz, ys, st);  // [ys][nz][nx] -> [nz][ys][nx]
     SD_HIP(hipMemcpy2DAsync(out + y0 * nx, size_t(ny * nx) * 4, tmp.p, size_t(ys * nx) * 4, size_t(ys * nx) * 4,
-                            size_t(nz), hipMemcpyDeviceToHost, st));
+                            size_t(nz), hipMemcpyDefault, st));
 }
 
 HostKernel Session::internal_kernel(const HostKernel& k) const {

@@ -31,8 +31,18 @@ def compute(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, local
             keep_intensity: bool = False, device: int = 0, ij_threads: int = 8,
             return_dog: bool = False, max_peaks: int | None = None):
     """ProcessDOG.compute: returns the list of InterestPoint (and the DoG image
-    when ``return_dog``).  ``img`` is a [z, y, x] float32 volume (not modified)."""
+    when ``return_dog``).  ``img`` is a [z, y, x] float32 volume (not modified):
+    a numpy array, or a torch tensor on the GPU -- a view already resident in HBM
+    is read in place (the returned DoG image is then a torch tensor too)."""
     lib = _lib.load()
+    on_dev = hasattr(img, "is_cuda") and img.is_cuda
+    if on_dev:
+        img = img.contiguous().float()
+        if img.dim() != 3:
+            raise ValueError("img must be 3D [z, y, x]")
+        return _compute_device(lib, img, sigma, threshold, localization, image_sigma, find_min, find_max,
+                               min_intensity, max_intensity, keep_intensity, device, ij_threads, return_dog,
+                               max_peaks)
     img = np.ascontiguousarray(img, np.float32)
     if img.ndim != 3:
         raise ValueError("img must be 3D [z, y, x]")
@@ -66,6 +76,70 @@ def compute(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, local
         out.append(InterestPoint(i, (ip.pos[0], ip.pos[1], ip.pos[2]),
                                  float(ip.intensity) if keep_intensity else None))
     return (out, dog) if return_dog else out
+
+
+def _params(lib, sigma, threshold, localization, image_sigma, find_min, find_max, min_intensity, max_intensity,
+            device, ij_threads):
+    p = _lib.DogParams()
+    lib.spim_dog_params_default(C.byref(p))
+    p.sigma, p.threshold, p.localization = float(sigma), float(threshold), int(localization)
+    for d in range(3):
+        p.image_sigma[d] = float(image_sigma[d])
+    p.find_min, p.find_max = int(bool(find_min)), int(bool(find_max))
+    p.min_intensity, p.max_intensity = float(min_intensity), float(max_intensity)
+    p.ij_threads, p.device = int(ij_threads), int(device)
+    return p
+
+
+# InterestPointC as a numpy record (pos: 3 doubles, intensity float, is_max int32)
+IP_DTYPE = np.dtype([("pos", "<f8", (3,)), ("intensity", "<f4"), ("is_max", "<i4")])
+
+
+def _points_device(lib, img, p, dog):
+    """spim_dog_interest_points on a GPU tensor: a numpy IP_DTYPE record array."""
+    import torch
+    torch.cuda.synchronize(img.device)   # the library runs on its own stream
+    dims = (C.c_int64 * 3)(img.shape[2], img.shape[1], img.shape[0])
+    fp = C.POINTER(C.c_float)
+    iptr = C.cast(C.c_void_p(img.data_ptr()), fp)
+    dptr = C.cast(C.c_void_p(dog.data_ptr()), fp) if dog is not None else None
+    cap = max(1 << 16, img.numel() // 512)   # room for a dense bead field: no second pass
+    n = C.c_int64(0)
+    while True:
+        buf = np.empty(cap, IP_DTYPE)
+        check(lib.spim_dog_interest_points(iptr, dims, C.byref(p), dptr,
+                                           buf.ctypes.data_as(C.POINTER(_lib.InterestPointC)), cap, C.byref(n)))
+        if int(n.value) <= cap:
+            return buf[:int(n.value)]
+        cap = int(n.value)
+
+
+def _compute_device(lib, img, sigma, threshold, localization, image_sigma, find_min, find_max, min_intensity,
+                    max_intensity, keep_intensity, device, ij_threads, return_dog, max_peaks):
+    import torch
+    p = _params(lib, sigma, threshold, localization, image_sigma, find_min, find_max, min_intensity,
+                max_intensity, device, ij_threads)
+    dog = torch.empty_like(img) if return_dog else None
+    rec = _points_device(lib, img, p, dog)
+    if max_peaks is not None:
+        rec = rec[:int(max_peaks)]
+    out = [InterestPoint(i, tuple(r["pos"].tolist()), float(r["intensity"]) if keep_intensity else None)
+           for i, r in enumerate(rec)]
+    return (out, dog) if return_dog else out
+
+
+def interest_points_array(img, sigma: float = 1.8, threshold: float = 0.008, localization: int = 0,
+                          image_sigma=(0.5, 0.5, 0.5), find_min: bool = False, find_max: bool = True,
+                          min_intensity: float = float("nan"), max_intensity: float = float("nan"),
+                          device: int = 0, ij_threads: int = 8):
+    """ProcessDOG.compute on a GPU tensor, as arrays: (positions (n, 3) x, y, z;
+    intensities (n,)) in the reference's order -- no per-point Python objects."""
+    lib = _lib.load()
+    img = img.contiguous().float()
+    p = _params(lib, sigma, threshold, localization, image_sigma, find_min, find_max, min_intensity,
+                max_intensity, device, ij_threads)
+    rec = _points_device(lib, img, p, None)
+    return np.ascontiguousarray(rec["pos"]), np.ascontiguousarray(rec["intensity"])
 
 
 def simple_peaks(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, localization: int = 0,

@@ -1,0 +1,138 @@
+"""One timepoint of the multiview pipeline, device resident (BASELINE configs[3]).
+
+The Fiji workflow the reference runs per timepoint, restated over this library:
+
+  1. Detect Interest Points   ProcessDOG.compute per view (spim/process/interestpointdetection/
+                              ProcessDOG.java:40-178) -> bead positions in view pixels
+  2. Register                 out of scope (GlobalOpt and descriptor matching run on the CPU,
+                              SURVEY 8f): the view models are given; the correspondences the
+                              registration would record are recovered from them (a detection
+                              corresponds when another view detected a bead within ``radius``
+                              world pixels of it)
+  3. Input preparation        ProcessForDeconvolution.fuseStacksAndGetPSFs (:159-384): views
+                              resampled into the bounding box, blending weights normalised,
+                              and per view the PSF extracted from its corresponding beads
+                              (getLocationsOfCorrespondingBeads :444-462, ExtractPSF.
+                              extractNextImg :260-279) and transformed with the view model
+  4. Deconvolution            MVDeconvolution (EfficientBayesianBased.java:166-286 defaults:
+                              OPTIMIZATION_I, lambda 0.006)
+
+Every volume stays in HBM (torch tensors are only device-memory plumbing); the
+stages are the library's C-ABI calls.  ``process_timepoint`` returns psi as a
+torch tensor and per-stage wall times.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib, dog, input_prep, psf as psf_mod
+from .decon import PSFTYPE, Session
+
+
+@dataclass
+class TimepointResult:
+    psi: object                              # torch tensor [z, y, x] on the GPU
+    points: list                             # per view: (n, 3) detections, view pixels (x, y, z)
+    corresponding: list                      # per view: indices of detections with a correspondence
+    psfs: list                               # per view: transformed PSF [z, y, x] (numpy)
+    stats: np.ndarray                        # RL (iterations, views, 2)
+    ms: dict = field(default_factory=dict)   # stage wall times
+    engine: dict = field(default_factory=dict)   # RL FFT dims and z / x pass modes
+
+
+def apply_model(model, pts):
+    """AffineTransform3D.apply for (n, 3) points (x, y, z)."""
+    m = np.asarray(model, np.float64).reshape(3, 4)
+    return np.asarray(pts, np.float64) @ m[:, :3].T + m[:, 3]
+
+
+def corresponding_detections(points, models, radius: float = 2.0):
+    """The detections of each view that lie within ``radius`` world pixels of a
+    detection of another view: the set ``getLocationsOfCorrespondingBeads`` reads
+    from the registration's correspondence lists (ProcessForDeconvolution.java:444-462)."""
+    from scipy.spatial import cKDTree
+    world = [apply_model(m, p) if len(p) else np.zeros((0, 3)) for p, m in zip(points, models)]
+    allp = np.concatenate(world)
+    label = np.concatenate([np.full(len(w), v) for v, w in enumerate(world)] + [np.array([-1])])
+    n = len(allp)
+    if n == 0:
+        return [np.zeros(0, np.int64) for _ in world]
+    # one tree over every view's detections; a detection corresponds when one of its
+    # 3 nearest other detections within the radius belongs to another view
+    k = min(4, n)
+    workers = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))   # the host's CPU share
+    _, idx = cKDTree(allp).query(allp, k=k, distance_upper_bound=radius, workers=workers)
+    idx = idx.reshape(n, k)
+    own = label[:n, None]
+    hit = ((label[idx] != own) & (idx < n)).any(axis=1)
+    out, o = [], 0
+    for w in world:
+        out.append(np.nonzero(hit[o:o + len(w)])[0])
+        o += len(w)
+    return out
+
+
+def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), iterations: int = 10,
+                      psftype: PSFTYPE = PSFTYPE.OPTIMIZATION_I, lam: float = 0.006, sigma: float = 1.8,
+                      threshold: float = 0.008, localization: int = 1, radius: float = 2.0,
+                      blending_border=(-8, -8, -8), blending_range=(12, 12, 12),
+                      weight_type=input_prep.WeightType.VIRTUAL_WEIGHTS, device: int = 0,
+                      log=None) -> TimepointResult:
+    """views: per view a [z, y, x] float32 torch tensor on the GPU (the acquired
+    stack); models: 3x4 view -> world affines; bb_min / bb_dims (x, y, z)."""
+    import torch
+    ms = {}
+
+    def lap(name, t0):
+        torch.cuda.synchronize(device)
+        ms[name] = round((time.perf_counter() - t0) * 1e3, 2)
+        if log:
+            log(f"{name}: {ms[name]} ms")
+        return time.perf_counter()
+
+    torch.cuda.synchronize(device)
+    t = time.perf_counter()
+    points = []
+    for v in views:          # 1. ProcessDOG per view, read in place
+        pos, _ = dog.interest_points_array(v, sigma=sigma, threshold=threshold, localization=localization,
+                                           device=device)
+        points.append(pos)
+    t = lap("detect", t)
+    corr = corresponding_detections(points, models, radius)   # 2. (registration given)
+    t = lap("correspondences", t)
+    imgs, ws, info = input_prep.prepare_inputs(views, models, bb_min, bb_dims, blending_border, blending_range,
+                                               weight_type, device=device)   # 3a.
+    t = lap("prepare_inputs", t)
+    psfs = []
+    for v, m, p, c in zip(views, models, points, corr):       # 3b. ExtractPSF from corresponding beads
+        # (a view with no corresponding bead -- registration would have failed for it --
+        # takes all of its detections rather than an all-zero PSF)
+        _, tr = psf_mod.extract_psf(v, p[c] if len(c) else p, psf_size, m, device=device)
+        psfs.append(tr)
+    t = lap("extract_psf", t)
+    shape = tuple(imgs[0].shape)
+    sess = Session((shape[2], shape[1], shape[0]), device=device)            # 4. MVDeconvolution
+    try:
+        for i, w, k in zip(imgs, ws, psfs):
+            sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
+        sess.init(psftype)
+        sess.init_psi()
+        engine = {"fft_dims_xyz": list(sess.fft_dims(0)), "zpass_mode": sess.zpass_mode(0),
+                  "kernel_planes": sess.kernel_planes(0)}
+        t = lap("rl_setup", t)
+        stats = sess.run(iterations, lam)
+        engine["xpass_mode"] = sess.xpass_mode(0)
+        sess.apply_mask()
+        t = lap("rl_iterations", t)
+        psi = torch.empty(shape, dtype=torch.float32, device=imgs[0].device)
+        _lib.check(sess.lib.mvd_get_psi(sess.h, C.cast(C.c_void_p(psi.data_ptr()), _lib._pf)))
+    finally:
+        sess.close()
+    del imgs, ws
+    lap("rl_result", t)
+    return TimepointResult(psi, points, corr, psfs, stats, ms, engine)

@@ -163,3 +163,97 @@ def make_views_torch(shape, num_views: int, config_id: int = 1, ksize=(25, 25, 2
     ws = [(w / wsum.clamp(min=1.0)).contiguous() for w in ws]
     del ft, tp, truth
     return imgs, ws, psfs
+
+
+def rotation_about_y(angle_deg: float, center_world, center_local):
+    """3x4 view -> world affine: a rotation about the y axis through the world
+    centre, mapping the local stack centre onto it (SPIM angles)."""
+    a = math.radians(angle_deg)
+    R = np.array([[math.cos(a), 0.0, math.sin(a)], [0.0, 1.0, 0.0], [-math.sin(a), 0.0, math.cos(a)]])
+    m = np.zeros((3, 4))
+    m[:, :3] = R
+    m[:, 3] = np.asarray(center_world, np.float64) - R @ np.asarray(center_local, np.float64)
+    return m
+
+
+def make_timepoint_torch(world_xyz, view_xyz, num_views: int, timepoint: int = 0, config_id: int = 4,
+                         psf_sigma=(1.2, 1.2, 3.0), photons: float = 1000.0, bead_density=1.0 / 20 ** 3,
+                         drift=(1.5, 0.5, 1.0), device="cuda", log=None):
+    """One timepoint of a multiview acquisition (BASELINE configs[3]) generated on
+    the GPU: a world volume of beads (3x3x3 footprint, drifting by ``drift`` pixels
+    per timepoint) and smooth blobs; view v is that volume seen through a rotation
+    about y by v * 360 / V degrees (trilinear resampling), blurred with an
+    axis-aligned Gaussian PSF in its own frame (sigma x, y, z), with Poisson noise.
+    Returns (views: list of [z, y, x] torch tensors, models: list of 3x4 view ->
+    world affines)."""
+    import torch
+    import torch.nn.functional as F
+
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED0 + 1000 * int(config_id))      # the same beads at every timepoint ...
+    wx, wy, wz = (int(v) for v in world_xyz)
+    z = torch.arange(wz, device=dev, dtype=torch.float32).view(-1, 1, 1)
+    y = torch.arange(wy, device=dev, dtype=torch.float32).view(1, -1, 1)
+    x = torch.arange(wx, device=dev, dtype=torch.float32).view(1, 1, -1)
+    truth = torch.zeros((wz, wy, wx), device=dev)
+    s = min(wx, wy, wz) / 8.0
+    for _ in range(6):
+        c = torch.rand(3, generator=g, device=dev) * torch.tensor([wz, wy, wx], device=dev, dtype=torch.float32)
+        truth += 0.2 * torch.exp(-0.5 * ((z - c[0]) ** 2 + (y - c[1]) ** 2 + (x - c[2]) ** 2) / s ** 2)
+    nb = max(1, int(wx * wy * wz * bead_density))
+    pos = torch.rand((nb, 3), generator=g, device=dev) * torch.tensor([wz - 8, wy - 8, wx - 8], device=dev,
+                                                                       dtype=torch.float32) + 4
+    pos = pos + torch.tensor([drift[2], drift[1], drift[0]], device=dev) * timepoint   # ... drifting
+    ip = pos.round().long()
+    ok = ((ip >= 1) & (ip < torch.tensor([wz - 1, wy - 1, wx - 1], device=dev))).all(dim=1)
+    ip = ip[ok]
+    amp = 0.5 + 0.5 * torch.rand(len(ip), generator=g, device=dev)
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                f = 0.55 ** (abs(dx) + abs(dy) + abs(dz))
+                idx = ((ip[:, 0] + dz) * wy + ip[:, 1] + dy) * wx + ip[:, 2] + dx
+                truth.view(-1).index_add_(0, idx, amp * f)
+    vx, vy, vz = (int(v) for v in view_xyz)
+    cw = ((wx - 1) / 2.0, (wy - 1) / 2.0, (wz - 1) / 2.0)
+    cl = ((vx - 1) / 2.0, (vy - 1) / 2.0, (vz - 1) / 2.0)
+    sx, sy, sz = psf_sigma
+
+    views, models = [], []
+    gv = torch.Generator(device=dev)
+    gv.manual_seed(SEED0 + 1000 * int(config_id) + 17 * int(timepoint) + 1)
+    for v in range(num_views):
+        if log:
+            log(f"  view {v}")
+        m = rotation_about_y(v * 360.0 / num_views, cw, cl)
+        models.append(m)
+        M = torch.tensor(m, device=dev, dtype=torch.float32)
+        out = torch.empty((vz, vy, vx), device=dev)
+        zs = max(1, (1 << 26) // (vx * vy))          # resample in z chunks (bounded grid memory)
+        for z0 in range(0, vz, zs):
+            z1 = min(vz, z0 + zs)
+            lz = torch.arange(z0, z1, device=dev, dtype=torch.float32).view(-1, 1, 1)
+            ly = torch.arange(vy, device=dev, dtype=torch.float32).view(1, -1, 1)
+            lx = torch.arange(vx, device=dev, dtype=torch.float32).view(1, 1, -1)
+            px = M[0, 0] * lx + M[0, 1] * ly + M[0, 2] * lz + M[0, 3]
+            py = M[1, 0] * lx + M[1, 1] * ly + M[1, 2] * lz + M[1, 3]
+            pz = M[2, 0] * lx + M[2, 1] * ly + M[2, 2] * lz + M[2, 3]
+            grid = torch.stack([2 * px / (wx - 1) - 1, 2 * py / (wy - 1) - 1, 2 * pz / (wz - 1) - 1], dim=-1)
+            out[z0:z1] = F.grid_sample(truth[None, None], grid[None], mode="bilinear", padding_mode="zeros",
+                                       align_corners=True)[0, 0]
+            del px, py, pz, grid
+        # Gaussian blur in the view's own frame: one FFT multiply by the separable
+        # transfer function (circular boundary -- synthetic data)
+        fz = torch.fft.fftfreq(vz, device=dev).view(-1, 1, 1)
+        fy = torch.fft.fftfreq(vy, device=dev).view(1, -1, 1)
+        fx = torch.fft.rfftfreq(vx, device=dev).view(1, 1, -1)
+        tf = torch.exp(-2.0 * math.pi ** 2 * ((fx * sx) ** 2 + (fy * sy) ** 2 + (fz * sz) ** 2))
+        out = torch.fft.irfftn(torch.fft.rfftn(out) * tf, s=(vz, vy, vx)).float()
+        del tf
+        lam = (photons * out + 5.0).clamp_(min=0.0)
+        img = (torch.poisson(lam, generator=gv) / photons).float().contiguous()
+        views.append(img)
+        del out, lam
+    del truth
+    return views, models

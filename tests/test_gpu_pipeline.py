@@ -1,0 +1,68 @@
+"""GPU: one timepoint of the multiview pipeline (BASELINE configs[3] chain:
+DoG detection -> correspondences -> input preparation + PSF extraction -> RL),
+device resident, checked stage by stage against the oracle on the same inputs."""
+import numpy as np
+import pytest
+import torch  # before the library loads (one shared HIP runtime)
+
+from conftest import rel_l2
+from oracle import dog_ref, input_ref, mvdecon_ref as ref, psf_ref
+from spim_registration_amd import input_prep, pipeline, synthetic
+from spim_registration_amd.decon import PSFTYPE
+
+pytestmark = pytest.mark.gpu
+
+WORLD = (48, 44, 40)
+PSF_SIZE = (9, 9, 11)
+
+
+@pytest.fixture(scope="module")
+def timepoint(gpu):
+    views, models = synthetic.make_timepoint_torch(WORLD, WORLD, 4, timepoint=1, config_id=41,
+                                                   bead_density=1.0 / 9 ** 3, device="cuda:0")
+    res = pipeline.process_timepoint(views, models, (0, 0, 0), WORLD, psf_size=PSF_SIZE, iterations=3)
+    return views, models, res
+
+
+def test_pipeline_detection_matches_oracle(timepoint):
+    views, models, res = timepoint
+    for v, img in enumerate(views):
+        exp, _ = dog_ref.process_dog(img.cpu().numpy(), 1.8, 0.008, localization=1)
+        assert len(exp) > 5
+        np.testing.assert_allclose(res.points[v], np.array([e[:3] for e in exp]), rtol=0, atol=1e-5)
+
+
+def test_pipeline_correspondences(timepoint):
+    views, models, res = timepoint
+    assert all(len(c) > 3 for c in res.corresponding)
+    # each corresponding detection has a detection of another view within the radius
+    world = [pipeline.apply_model(m, p) for p, m in zip(res.points, models)]
+    for v, c in enumerate(res.corresponding):
+        others = np.concatenate([w for u, w in enumerate(world) if u != v])
+        d = np.linalg.norm(world[v][c][:, None, :] - others[None], axis=-1).min(axis=1)
+        assert (d <= 2.0).all()
+
+
+def test_pipeline_psfs_match_oracle(timepoint):
+    views, models, res = timepoint
+    for v, img in enumerate(views):
+        locs = res.points[v][res.corresponding[v]]
+        _, want = psf_ref.extract_next_img(img.cpu().numpy(), models[v], locs, PSF_SIZE)
+        np.testing.assert_allclose(res.psfs[v], want, rtol=1e-5, atol=1e-6)
+
+
+def test_pipeline_inputs_and_rl_match_oracle(timepoint):
+    views, models, res = timepoint
+    imgs, ws, _ = input_prep.prepare_inputs(views, models, (0, 0, 0), WORLD, (-8, -8, -8), (12, 12, 12))
+    hv = [v.cpu().numpy() for v in views]
+    ei, ew, _ = input_ref.prepare_inputs(hv, models, (0, 0, 0), WORLD, (-8, -8, -8), (12, 12, 12))
+    hi = [i.cpu().numpy() for i in imgs]
+    hw = [w.cpu().numpy() for w in ws]
+    for v in range(len(views)):
+        np.testing.assert_allclose(hi[v], ei[v], rtol=1e-5, atol=1e-6)   # 90-degree models: no ties
+        np.testing.assert_allclose(hw[v], ew[v], rtol=1e-5, atol=1e-6)
+    # RL on the library's own prepared inputs and PSFs (OPTIMIZATION_I, lambda 0.006)
+    want = ref.mv_deconvolution(hi, hw, res.psfs, PSFTYPE.OPTIMIZATION_I, 3, 0.006).psi
+    got = res.psi.cpu().numpy()
+    assert np.isfinite(got).all() and (got > 0).mean() > 0.5
+    assert rel_l2(got, want) < 1e-4
