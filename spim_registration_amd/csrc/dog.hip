@@ -504,6 +504,44 @@ __device__ __forceinline__ void sink_append(const PeakSink& pk, bool flag, int x
     }
 }
 
+// Per-wave candidate buffer of k_dog_z: entries {x, y | sp << 30, z, bits(|c|)} collect in
+// LDS and go to the sink 64 at a time (one global atomic per flush instead of one per
+// wave-step with a candidate; its returned value is the only vmcnt(0) in the loop)
+constexpr int kCandBuf = 64;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void cand_flush(const PeakSink& pk, const int4* buf, int n, int nx, uint32_t pstride) {
+    if (n == 0) return;
+    wave_lds_sync();
+    const int lane = int(threadIdx.x & 63);
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(pk.count, unsigned(n));
+    base = unsigned(__shfl(int(base), 0, 64));
+    if (lane < n) {
+        const int4 e = buf[lane];
+        const unsigned pos = base + unsigned(lane);
+        if (pos < pk.cap) {
+            const int x = e.x, y = e.y & 0x3fffffff, sp = int(unsigned(e.y) >> 30), z = e.z;
+            pk.keys[pos] = (uint64_t(x % pk.T) << 40) | (uint64_t(z) * pstride + uint64_t(y) * uint32_t(nx) + x);
+            pk.vals[pos] = pos;
+            PeakOut o;
+            o.x = x;
+            o.y = y;
+            o.z = z;
+            o.intensity = __int_as_float(e.w);
+            o.is_min = sp == 1;
+            o.is_max = sp == 2;
+            pk.recs[pos] = o;
+        }
+    }
+    wave_lds_sync();   // the buffer is rewritten after the flush
+}
+
 // z Gaussians + DoG + peak test over one column box and one chunk of planes.  Each
 // thread keeps its column's window of KW planes (+ kDzPD loaded ahead) of (G1, G2) in
 // registers, rotating by unrolling; the DoG planes go through a 4-plane LDS ring.  The
@@ -518,6 +556,8 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
     constexpr int NW = KW + kDzPD;
     __shared__ float Dr[4][BY][kDzBX];
     __shared__ int nanq[4];
+    __shared__ int4 cbuf[BY][kCandBuf];   // one candidate buffer per wave (= row ty)
+    int ccount = 0;                       // wave-uniform fill of this wave's buffer
     const int t = threadIdx.x, tx = t & (kDzBX - 1), ty = t / kDzBX;
     const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
     const int X0 = int(blockIdx.x) * (kDzBX - 2), Y0 = int(blockIdx.y) * (BY - 2);
@@ -618,10 +658,22 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
                     sp = ge ? 2 : (le ? 1 : 0);
                 }
                 const bool flag = (sp == 2 && pk.want_max) || (sp == 1 && pk.want_min);
-                sink_append(pk, flag, x, y, zc, uint64_t(zc) * pstride + col, c, sp);
+                const unsigned long long bal = __ballot(flag);
+                if (bal != 0ull) {
+                    const int nb = __popcll(bal);
+                    if (ccount + nb > kCandBuf) {
+                        cand_flush(pk, cbuf[ty], ccount, nx, pstride);
+                        ccount = 0;
+                    }
+                    if (flag)
+                        cbuf[ty][ccount + __popcll(bal & ((1ull << (tx & 63)) - 1ull))] =
+                            make_int4(x, y | (sp << 30), zc, __float_as_int(fabsf(c)));
+                    ccount += nb;
+                }
             }
         }
     }
+    cand_flush(pk, cbuf[ty], ccount, nx, pstride);
 }
 
 __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in, int64_t n,

@@ -67,7 +67,8 @@ __global__ __launch_bounds__(kIpBlock) void k_transform_view(ViewArgs v, int64_t
                                                              float* __restrict__ w_out) {
     const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
     if (i >= n) return;
-    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    int64_t x, y, z;
+    flat_xyz(i, nx, ny, n, x, y, z);
     // TransformInput: s = (float) position + offset; t = inv3 (s - translation)
     const float s0 = float(x) + float(bx), s1 = float(y) + float(by), s2 = float(z) + float(bz);
     const double d0 = double(s0) - v.a.tr[0], d1 = double(s1) - v.a.tr[1], d2 = double(s2) - v.a.tr[2];
@@ -96,18 +97,25 @@ __global__ __launch_bounds__(kIpBlock) void k_transform_view(ViewArgs v, int64_t
 
 // WeightNormalizer: sum over views (double, view order), count of views with w > 0;
 // PRECOMPUTED: w /= sum in place; VIRTUAL: S = sum > 1 ? (float) sum : 1.
-// Overlap statistics per reference portion: atomic min of the count, atomic sum.
+// Overlap statistics per reference portion (grid.y = portion, grid.x = blocks striding
+// over it): per-thread min / sum of the counts, one atomic pair per block.
 __global__ __launch_bounds__(kIpBlock) void k_weight_sum(float* const* __restrict__ ws, int nviews, int64_t n,
                                                          int weight_type, float* __restrict__ S,
                                                          int64_t chunk, int nportions,
                                                          int* __restrict__ pmin,
                                                          unsigned long long* __restrict__ psum) {
-    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
-    int cnt = nviews;
-    int port = -1;
-    if (i < n) {
+    __shared__ int smin[kIpBlock / 64];
+    __shared__ unsigned long long ssum[kIpBlock / 64];
+    const int port = int(blockIdx.y);
+    // the last portion takes the remainder (all of it when size < portions)
+    const int64_t lo = chunk > 0 ? int64_t(port) * chunk : (port == nportions - 1 ? 0 : n);
+    const int64_t hi = port == nportions - 1 ? n : lo + chunk;
+    int m = nviews;
+    unsigned long long sm = 0ull;
+    for (int64_t i = lo + int64_t(blockIdx.x) * kIpBlock + threadIdx.x; i < hi;
+         i += int64_t(gridDim.x) * kIpBlock) {
         double sum = 0.0;
-        cnt = 0;
+        int cnt = 0;
         for (int v = 0; v < nviews; ++v) {
             const float w = ws[v][i];
             sum += w;
@@ -118,27 +126,25 @@ __global__ __launch_bounds__(kIpBlock) void k_weight_sum(float* const* __restric
         } else {
             S[i] = sum > 1.0 ? float(sum) : 1.0f;
         }
-        // the last portion takes the remainder (all of it when size < portions)
-        port = chunk > 0 ? int(i / chunk) : nportions - 1;
-        if (port >= nportions) port = nportions - 1;
+        m = min(m, cnt);
+        sm += (unsigned long long)cnt;
     }
-    // one atomic pair per wave when the wave lies in one portion (the common case)
-    const int p0 = __shfl(port, 0, 64);
-    const bool uniform = __all(port == p0 || port < 0);
-    if (uniform && p0 >= 0) {
-        int m = port >= 0 ? cnt : nviews;
-        unsigned long long sm = port >= 0 ? (unsigned long long)cnt : 0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            m = min(m, __shfl_xor(m, off, 64));
-            sm += __shfl_xor(sm, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        m = min(m, __shfl_xor(m, off, 64));
+        sm += __shfl_xor(sm, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        smin[threadIdx.x >> 6] = m;
+        ssum[threadIdx.x >> 6] = sm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && lo < hi) {
+        for (int w = 1; w < kIpBlock / 64; ++w) {
+            m = min(m, smin[w]);
+            sm += ssum[w];
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&pmin[p0], m);
-            atomicAdd(&psum[p0], sm);
-        }
-    } else if (!uniform && port >= 0) {
-        atomicMin(&pmin[port], cnt);
-        atomicAdd(&psum[port], (unsigned long long)cnt);
+        atomicMin(&pmin[port], m);
+        atomicAdd(&psum[port], sm);
     }
 }
 
@@ -179,7 +185,8 @@ __global__ __launch_bounds__(kIpBlock) void k_fuse(const FuseView* __restrict__ 
                                                    float* __restrict__ out) {
     const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
     if (i >= n) return;
-    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    int64_t x, y, z;
+    flat_xyz(i, nx, ny, n, x, y, z);
     float f0 = float(x), f1 = float(y), f2 = float(z);
     if (ds != 1.0f) {
         f0 = f0 * ds;
@@ -301,8 +308,10 @@ void prepare_inputs(int nviews, const spim_view_source* views, const spim_input_
         std::vector<int> hmin(np, nviews);
         SD_HIP(hipMemcpyAsync(pmin.p, hmin.data(), np * 4, hipMemcpyHostToDevice, s));
         SD_HIP(hipMemsetAsync(psum.p, 0, np * 8, s));
-        hipLaunchKernelGGL(k_weight_sum, dim3(grid), dim3(kIpBlock), 0, s, dws.p, nviews, n, p->weight_type, S.p,
-                           n / np, np, pmin.p, psum.p);
+        const int64_t span = std::max<int64_t>(n / np, n - (n / np) * (np - 1));   // the largest portion
+        const unsigned bx = unsigned(std::max<int64_t>(1, std::min<int64_t>(ceil_div(span, kIpBlock), 8192 / np)));
+        hipLaunchKernelGGL(k_weight_sum, dim3(bx, unsigned(np)), dim3(kIpBlock), 0, s, dws.p, nviews, n,
+                           p->weight_type, S.p, n / np, np, pmin.p, psum.p);
         SD_HIP(hipGetLastError());
         std::vector<unsigned long long> hsum(np);
         SD_HIP(hipMemcpyAsync(hmin.data(), pmin.p, np * 4, hipMemcpyDeviceToHost, s));

@@ -57,6 +57,20 @@ __device__ float nlinear_at(const float* src, int sx, int sy, int sz, double p0,
     const int xb = xa + 1, yb = ya + 1, zb = za + 1;
     const double w0 = p0 - f0, w1 = p1 - f1, w2 = p2 - f2;
     const double i0 = 1.0 - w0, i1 = 1.0 - w1, i2 = 1.0 - w2;
+    if (xa >= 0 && ya >= 0 && za >= 0 && xb < sx && yb < sy && zb < sz) {
+        // every corner inside: one base index, no per-corner extension arithmetic
+        const float* b = src + (int64_t(za) * sy + ya) * sx + xa;
+        const int64_t py = sx, pz = int64_t(sx) * sy;
+        float acc = float(double(b[0]) * (i0 * i1 * i2));
+        acc = acc + float(double(b[1]) * (w0 * i1 * i2));
+        acc = acc + float(double(b[py + 1]) * (w0 * w1 * i2));
+        acc = acc + float(double(b[py]) * (i0 * w1 * i2));
+        acc = acc + float(double(b[pz + py]) * (i0 * w1 * w2));
+        acc = acc + float(double(b[pz + py + 1]) * (w0 * w1 * w2));
+        acc = acc + float(double(b[pz + 1]) * (w0 * i1 * w2));
+        acc = acc + float(double(b[pz]) * (i0 * i1 * w2));
+        return acc;
+    }
     auto at = [&](int x, int y, int z) { return double(ext_at<EXT>(src, sx, sy, sz, x, y, z)); };
     float acc = float(at(xa, ya, za) * (i0 * i1 * i2));
     acc = acc + float(at(xb, ya, za) * (w0 * i1 * i2));
@@ -67,6 +81,23 @@ __device__ float nlinear_at(const float* src, int sx, int sy, int sz, double p0,
     acc = acc + float(at(xb, ya, zb) * (w0 * i1 * w2));
     acc = acc + float(at(xa, ya, zb) * (i0 * i1 * w2));
     return acc;
+}
+
+// (x, y, z) of a flat x-fastest index: 32-bit divisions when the volume allows
+// (a 64-bit division is a ~100-instruction software routine on the GPU)
+__device__ __forceinline__ void flat_xyz(int64_t i, int64_t nx, int64_t ny, int64_t n, int64_t& x, int64_t& y,
+                                         int64_t& z) {
+    if (n < (int64_t(1) << 32)) {
+        const uint32_t ii = uint32_t(i), ux = uint32_t(nx), uy = uint32_t(ny);
+        const uint32_t q = ii / ux;
+        x = ii - q * ux;
+        z = q / uy;
+        y = q - uint32_t(z) * uy;
+    } else {
+        x = i % nx;
+        y = (i / nx) % ny;
+        z = i / (nx * ny);
+    }
 }
 
 inline AffineInv invert_model(const double* m) {

@@ -24,7 +24,6 @@ torch tensor and per-stage wall times.
 from __future__ import annotations
 
 import ctypes as C
-import os
 import time
 from dataclasses import dataclass, field
 
@@ -51,29 +50,46 @@ def apply_model(model, pts):
     return np.asarray(pts, np.float64) @ m[:, :3].T + m[:, 3]
 
 
-def corresponding_detections(points, models, radius: float = 2.0):
+def corresponding_detections(points, models, radius: float = 2.0, device=None):
     """The detections of each view that lie within ``radius`` world pixels of a
     detection of another view: the set ``getLocationsOfCorrespondingBeads`` reads
-    from the registration's correspondence lists (ProcessForDeconvolution.java:444-462)."""
-    from scipy.spatial import cKDTree
+    from the registration's correspondence lists (ProcessForDeconvolution.java:444-462).
+
+    All pairs within the radius are found exactly through a hash of radius-sized
+    cells (sorted cell keys, the 27 neighbouring cells of each point looked up by
+    binary search), in torch on ``device`` (the GPU in the pipeline, the CPU in
+    the host tests)."""
+    import torch
+    dev = torch.device(device if device is not None else "cpu")
     world = [apply_model(m, p) if len(p) else np.zeros((0, 3)) for p, m in zip(points, models)]
-    allp = np.concatenate(world)
-    label = np.concatenate([np.full(len(w), v) for v, w in enumerate(world)] + [np.array([-1])])
-    n = len(allp)
+    sizes = [len(w) for w in world]
+    n = sum(sizes)
     if n == 0:
         return [np.zeros(0, np.int64) for _ in world]
-    # one tree over every view's detections; a detection corresponds when one of its
-    # 3 nearest other detections within the radius belongs to another view
-    k = min(4, n)
-    workers = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))   # the host's CPU share
-    _, idx = cKDTree(allp).query(allp, k=k, distance_upper_bound=radius, workers=workers)
-    idx = idx.reshape(n, k)
-    own = label[:n, None]
-    hit = ((label[idx] != own) & (idx < n)).any(axis=1)
+    P = torch.from_numpy(np.concatenate(world)).to(dev, torch.float64)
+    lab = torch.cat([torch.full((k,), v, dtype=torch.int64) for v, k in enumerate(sizes)]).to(dev)
+    cell = torch.floor(P / radius).to(torch.int64)
+    cell = cell - cell.min(dim=0).values + 1
+    dims = cell.max(dim=0).values + 2
+    key = (cell[:, 0] * dims[1] + cell[:, 1]) * dims[2] + cell[:, 2]
+    skey, order = torch.sort(key)
+    Ps, Ls = P[order], lab[order]
+    r2 = float(radius) ** 2
+    offs = torch.tensor([(dx * dims[1] + dy) * dims[2] + dz for dx in (-1, 0, 1) for dy in (-1, 0, 1)
+                         for dz in (-1, 0, 1)], dtype=torch.int64, device=dev)
+    nk = key[None, :] + offs[:, None]                          # [27, n] neighbouring cell keys
+    lo = torch.searchsorted(skey, nk, side="left")
+    cnt = torch.searchsorted(skey, nk, side="right") - lo
+    hit = torch.zeros(n, dtype=torch.bool, device=dev)
+    for j in range(int(cnt.max())):                            # (a cell rarely holds more than 2)
+        idx = (lo + j).clamp(max=n - 1)
+        d2 = ((Ps[idx] - P[None]) ** 2).sum(dim=2)
+        hit |= ((j < cnt) & (Ls[idx] != lab[None]) & (d2 <= r2)).any(dim=0)
+    hit = hit.cpu().numpy()
     out, o = [], 0
-    for w in world:
-        out.append(np.nonzero(hit[o:o + len(w)])[0])
-        o += len(w)
+    for k in sizes:
+        out.append(np.nonzero(hit[o:o + k])[0])
+        o += k
     return out
 
 
@@ -103,7 +119,7 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
                                            device=device)
         points.append(pos)
     t = lap("detect", t)
-    corr = corresponding_detections(points, models, radius)   # 2. (registration given)
+    corr = corresponding_detections(points, models, radius, device=f"cuda:{device}")   # 2. (registration given)
     t = lap("correspondences", t)
     imgs, ws, info = input_prep.prepare_inputs(views, models, bb_min, bb_dims, blending_border, blending_range,
                                                weight_type, device=device)   # 3a.

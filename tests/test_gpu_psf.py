@@ -71,3 +71,18 @@ def test_average_transformed_psf_and_max_projection(gpu):
         want, wused = pr.max_projection(a, d)
         assert used == wused
         np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("nbeads", [65, 300])
+def test_extract_psf_many_beads_two_phase(gpu, nbeads):
+    """More than 64 beads: all (bead, voxel) samples in parallel, then each voxel's
+    float sum in bead order -- the same bits as the per-voxel loop and the oracle."""
+    img, _ = bead_view(cid=23)
+    rng = np.random.default_rng(nbeads)
+    locs = rng.uniform([0, 0, 0], [64, 56, 40], size=(nbeads, 3))
+    few = psf.extract_psf(img, locs[:64], (9, 9, 11), ROT)[0]          # per-voxel loop path
+    orig, trans = psf.extract_psf(img, locs, (9, 9, 11), ROT)
+    eo, et = pr.extract_next_img(img, ROT, locs, (9, 9, 11))
+    np.testing.assert_allclose(orig, eo, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(trans, et, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(few, pr.extract_next_img(img, ROT, locs[:64], (9, 9, 11))[0], rtol=1e-6, atol=1e-7)

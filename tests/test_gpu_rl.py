@@ -38,6 +38,20 @@ def test_prepare_kernels_matches_oracle(gpu, psftype):
         assert rel_l2(a, b) < 1e-5
 
 
+@pytest.mark.parametrize("psftype", [PSFTYPE.OPTIMIZATION_I, PSFTYPE.OPTIMIZATION_II])
+def test_prepare_kernels_large_compound(gpu, psftype):
+    """Kernels of 45-degree-transformed PSFs (31 x 19 x 31): the compound convolutions
+    split each output's taps over a block (k_conv_same_zero_blk)."""
+    ks = [synthetic.psf(v, 4, (31, 19, 31)) for v in range(3)] + [synthetic.psf(3, 4, (25, 19, 21))]
+    views = [MVDeconFFT(np.ones((4, 4, 4)), np.ones((4, 4, 4)), k) for k in ks]
+    k1, k2 = prepare_kernels(views, psftype, ij_threads=8)
+    r1, r2 = ref.prepare_kernels(ks, psftype, 8)
+    for a, b in zip(k1, r1):
+        assert rel_l2(a, b) < 1e-6
+    for a, b in zip(k2, r2):
+        assert rel_l2(a, b) < 1e-5
+
+
 @pytest.mark.parametrize("T", [1, 3, 8])
 def test_norm_quirk_thread_count(gpu, T):
     k = synthetic.psf(0, 1, (9, 9, 13))
