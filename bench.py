@@ -70,7 +70,7 @@ def parse():
 
 
 # engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
-PMC_KERNELS = {"z_convolve": ("k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
+PMC_KERNELS = {"z_convolve": ("k_zdma<", "k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
                "x_update": ("k_xtile<2,", "k_xrows<2,", "k_xpass<2,"),
                "x_quotient": ("k_xtile<1,", "k_xrows<1,", "k_xpass<1,")}
 
@@ -164,7 +164,7 @@ def main():
     if args.strong:      # the global volume is fixed; rank r owns slab r of N along the longer of y, z
         from spim_registration_amd.distributed import slab_range
         nz_g = nz
-        if ny > nz and world > 1:   # (1024x1024x512: 128 + 24 halo rows per rank, not 64 + 24 planes)
+        if ny > nz and (world > 1 or args.local_slabs > 1):   # (1024x1024x512: 128 + 24 halo rows per rank, not 64 + 24 planes)
             axis = "y"
             o0, o1 = slab_range(ny_g, world, rank)
             ny = o1 - o0

@@ -975,7 +975,12 @@ static int zdma_tx(int64_t Mz, int cz) {
     const int KC = zdirect_kc_bound(cz);
     const int64_t nz = Mz - 2 * cz;
     if (!zdma_enabled() || KC == 0 || nz < 1) return 0;
+    static const int force = [] {   // SPIMDECON_ZDMA_TX=8: 8-column tiles even when 16 fit (A/B runs)
+        const char* e = std::getenv("SPIMDECON_ZDMA_TX");
+        return e ? std::atoi(e) : 0;
+    }();
     for (int tx : {16, 8})
+        if (force != 8 || tx == 8)
         if (zdma_lds(Mz, nz, KC, zdma_opt(int(nz), KC, tx), tx) <= 160 * 1024) return tx;
     return 0;
 }
