@@ -7,6 +7,7 @@
 //   computeQuotient         spim/process/fusion/deconvolution/MVDeconvolution.java:473-525
 //   computeFinalValues      spim/process/fusion/deconvolution/MVDeconvolution.java:582-705
 #include "fftconv.hpp"
+#include "rl_math.hpp"
 
 #include <cmath>
 #include <cstdlib>
@@ -65,50 +66,10 @@ __device__ __forceinline__ float2 csub_mi(float2 a, float2 d) {
     return f2_(__builtin_elementwise_fma(D.yx, INV ? sd_v2{1.0f, -1.0f} : sd_v2{-1.0f, 1.0f}, v2_(a)));
 }
 
-__device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
-    if (n == 1) return 0;
-    const int64_t p = 2 * (n - 1);
-    int64_t j = s % p;
-    if (j < 0) j += p;
-    return j >= n ? p - j : j;
-}
-
 template <int S>
 __device__ __forceinline__ float ldv(const void* p, int64_t i) {
     if constexpr (S == 0) return static_cast<const float*>(p)[i];
     else return __half2float(static_cast<const __half*>(p)[i]);
-}
-
-// MVDeconvolution.computeNextValue (:671-703), float op order kept.
-__device__ __forceinline__ float next_value(float last, float integral, float weight, double lambda) {
-    const float value = __fmul_rn(last, integral);
-    float adjusted;
-    if (value > 0.0f) {
-        if (lambda > 0.0)
-            adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
-        else
-            adjusted = value;
-    } else {
-        adjusted = kMinValue;
-    }
-    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
-    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
-}
-
-// Same with lambda's sign known at compile time: the Tikhonov branch (double
-// sqrt / divide) is not even if-converted into the lambda = 0 kernels.
-template <bool TIK>
-__device__ __forceinline__ float next_value_t(float last, float integral, float weight, double lambda) {
-    const float value = __fmul_rn(last, integral);
-    float adjusted;
-    if (value > 0.0f) {
-        if constexpr (TIK) adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
-        else adjusted = value;
-    } else {
-        adjusted = kMinValue;
-    }
-    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
-    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
 }
 
 // ------------------------------------------------------------------ radix-R DFTs

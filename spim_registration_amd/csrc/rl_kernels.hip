@@ -10,6 +10,7 @@
 //   quotient  img > 0 ? img / blurred : 1             MVDeconvolution.java:473-525
 //   update    computeNextValue + Tikhonov (f64 sqrt)   MVDeconvolution.java:671-705
 #include "rl_kernels.hpp"
+#include "rl_math.hpp"
 
 #include <algorithm>
 
@@ -24,15 +25,6 @@ __device__ __forceinline__ int64_t s_of_q(int64_t q, int64_t n, int c, int64_t M
     return q < n + c ? q : q - M;
 }
 
-// extendMirrorSingle index (numpy 'reflect'), periodic for far coordinates
-__device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
-    if (n == 1) return 0;
-    const int64_t p = 2 * (n - 1);
-    int64_t j = s % p;
-    if (j < 0) j += p;
-    return j >= n ? p - j : j;
-}
-
 template <int S>
 __device__ __forceinline__ float ld(const void* p, int64_t i) {
     if constexpr (S == 0) {
@@ -40,22 +32,6 @@ __device__ __forceinline__ float ld(const void* p, int64_t i) {
     } else {
         return __half2float(static_cast<const __half*>(p)[i]);
     }
-}
-
-// MVDeconvolution.computeNextValue (:671-703), float op order kept.
-__device__ __forceinline__ float next_value(float last, float integral, float weight, double lambda) {
-    const float value = __fmul_rn(last, integral);
-    float adjusted;
-    if (value > 0.0f) {
-        if (lambda > 0.0)
-            adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
-        else
-            adjusted = value;
-    } else {
-        adjusted = kMinValue;
-    }
-    const float next = isnan(adjusted) ? kMinValue : fmaxf(kMinValue, adjusted);
-    return __fadd_rn(last, __fmul_rn(__fsub_rn(next, last), weight));
 }
 
 struct RowMap {
