@@ -274,6 +274,10 @@ def main():
             cnt = int(tm[8 + i])
             if not cnt:
                 continue
+            if nm == "y_pass" and args.backend == "engine":
+                # with a halo exchange the forward y pass runs as plane ranges around the
+                # exchange wait (3 launches): count whole-volume passes, 4 per view and slab
+                cnt = min(cnt, 4 * V * 2 * max(1, args.local_slabs))
             avg = tm[i] / cnt
             ent = {"total_ms": round(tm[i], 4), "launches": cnt, "avg_ms": round(avg, 5)}
             byts = bvox * nv + bspec * S

@@ -1040,6 +1040,15 @@ void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
     else launch_col<1, false, 0>(p, p.fy, C, nullptr, s);
 }
 
+bool engine_ypass_planes(const SpectralPlan& p, float2* C, int z0, int z1, hipStream_t s) {
+    if (!p.fy.n1 || z0 < 0 || z1 > int(p.g.Mz)) return false;  // Stockham passes: whole volume only
+    if (z1 <= z0) return true;
+    // the y transforms of one z plane touch that plane only: a plane range is the same
+    // pass over a shifted base
+    return launch_col2f<1, 0>(p, p.fy, C + size_t(z0) * size_t(p.g.My) * size_t(p.Hp), nullptr, s, 0, -1, 0,
+                              z1 - z0);
+}
+
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s) {
     // fused forward * K * inverse (0.57 ms at 540^3) beat forward z + (C*K) inverse z
     // as two launches (0.61 ms)

@@ -88,6 +88,9 @@ void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx,
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s);
 // Y pass: in-place complex FFT along y (inverse when inv)
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
+// Forward y pass of the z planes [z0, z1) only (false: not available for this plan,
+// run engine_ypass instead)
+bool engine_ypass_planes(const SpectralPlan& p, float2* C, int z0, int z1, hipStream_t s);
 // Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
 // y forward + z convolve + y inverse over bands of `band` tile columns (Infinity-Cache

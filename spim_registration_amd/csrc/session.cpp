@@ -804,19 +804,54 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             exchange(buffer_a, st);
         }
     };
-    auto convolve = [&](SlabState& sl, float2* Cb, const float2* K) {
-        if (band > 0) {
+    auto convolve = [&](SlabState& sl, float2* Cb, const float2* K, bool fwd_done) {
+        if (band > 0 && !fwd_done) {
             T0(7);
             const bool banded = engine_convolve_banded(sl.sp, Cb, K, sl.kcompact, band, st);
             T1();
             if (banded) return;
         }
-        T0(2); engine_ypass(sl.sp, Cb, false, st); T1();
+        if (!fwd_done) { T0(2); engine_ypass(sl.sp, Cb, false, st); T1(); }
         T0(3);
         if (sl.kcompact) engine_zpass_compact(sl.sp, Cb, K, st);
         else engine_zpass(sl.sp, Cb, K, st);
         T1();
         T0(2); engine_ypass(sl.sp, Cb, true, st); T1();
+    };
+    // Both convolutions of every slab, for buffer C1 (buffer_a) or C2 of view v.  With an
+    // exchange in flight (pending) the forward y pass of the planes nobody exchanges,
+    // [cz, nz - cz), runs before waiting for it: the neighbours still read my boundary
+    // planes [0, cz) and [nz - cz, nz) (the y pass works in place), and my halo planes
+    // [nz, Mz) are still arriving.
+    const int czx = halo_[2];
+    auto convolve_all = [&](bool buffer_a, int v, bool pending) {
+        auto buf = [&](SlabState& sl) { return buffer_a ? sl.C1.p : sl.C2.p; };
+        auto ker = [&](SlabState& sl) { return buffer_a ? sl.e1spec[v].p : sl.e2spec[v].p; };
+        bool split = pending && band <= 0;
+        for (int s = s0; s < s1 && split; ++s)
+            split = slabs_[s].sp.fy.n1 != 0 && int(slabs_[s].g.nz) > 2 * czx;
+        if (split) {
+            for (int s = s0; s < s1; ++s) {
+                SlabState& sl = slabs_[s];
+                T0(2);
+                SD_CHECK(engine_ypass_planes(sl.sp, buf(sl), czx, int(sl.g.nz) - czx, st), SPIMDECON_ERR_STATE,
+                         "y pass of a plane range not available");
+                T1();
+            }
+            xend();
+            for (int s = s0; s < s1; ++s) {
+                SlabState& sl = slabs_[s];
+                T0(2);
+                SD_CHECK(engine_ypass_planes(sl.sp, buf(sl), 0, czx, st) &&
+                             engine_ypass_planes(sl.sp, buf(sl), int(sl.g.nz) - czx, int(sl.g.Mz), st),
+                         SPIMDECON_ERR_STATE, "y pass of a plane range not available");
+                T1();
+            }
+            for (int s = s0; s < s1; ++s) convolve(slabs_[s], buf(slabs_[s]), ker(slabs_[s]), true);
+            return;
+        }
+        if (pending) xend();
+        for (int s = s0; s < s1; ++s) convolve(slabs_[s], buf(slabs_[s]), ker(slabs_[s]), false);
     };
 
     for (int s = s0; s < s1; ++s) {
@@ -825,10 +860,12 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
         T1();
     }
     xfull(true);
+    bool pending = false;  // the update's exchange of C1 is still in flight
     for (int it = 0; it < iters; ++it) {
         for (int v = 0; v < V; ++v) {
             const bool last = (it == iters - 1) && (v == V - 1);
-            for (int s = s0; s < s1; ++s) convolve(slabs_[s], slabs_[s].C1.p, slabs_[s].e1spec[v].p);
+            convolve_all(true, v, pending);
+            pending = false;
             // quotient (+ forward x of the quotient) and its halo exchange
             if (overlap) {
                 for (int s = s0; s < s1; ++s) {
@@ -840,7 +877,6 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                     SlabState& sl = slabs_[s];
                     T0(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, rest[s], st); T1();
                 }
-                xend();
             } else {
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
@@ -850,7 +886,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                 }
                 xfull(false);
             }
-            for (int s = s0; s < s1; ++s) convolve(slabs_[s], slabs_[s].C2.p, slabs_[s].e2spec[v].p);
+            convolve_all(false, v, overlap);
             // update (+ forward x of the next psi) and its halo exchange
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
@@ -879,7 +915,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                 T1();
                 std::swap(sl.psi, sl.psi_next);
             }
-            if (ov) xend();
+            if (ov) pending = true;  // ended inside the next view's convolve_all
             else if (!last) xfull(true);
         }
     }
