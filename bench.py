@@ -70,7 +70,7 @@ def parse():
 
 
 # engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
-PMC_KERNELS = {"z_convolve": ("k_zdma<", "k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
+PMC_KERNELS = {"z_convolve": ("k_zdmc<", "k_zdma<", "k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
                "x_update": ("k_xtile<2,", "k_xrows<2,", "k_xpass<2,"),
                "x_quotient": ("k_xtile<1,", "k_xrows<1,", "k_xpass<1,")}
 

@@ -33,6 +33,9 @@ namespace spimdecon {
 size_t peak_sort_temp_bytes(int64_t n, int end_bit);
 void peak_sort(void* tmp, size_t tmp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
                uint32_t* vout, int64_t n, int end_bit, hipStream_t s);
+size_t point_select_temp_bytes(int64_t n);
+void point_select(void* tmp, size_t tmp_bytes, const spim_interest_point* in, const unsigned char* flags,
+                  spim_interest_point* out, int* nsel, int64_t n, hipStream_t s);
 
 namespace {
 
@@ -1064,11 +1067,16 @@ struct DogWork {
     DBuf<PeakOut> recs, peaks;
     DBuf<unsigned> count;
     DBuf<unsigned char> sort_tmp;
+    DBuf<LocOut> loc;                      // localisation results
+    DBuf<spim_interest_point> ips, ips_sel;  // interest points before / after the threshold
+    DBuf<unsigned char> flags, sel_tmp;
+    DBuf<int> nsel;
     void release() {
         for (DBuf<float>* b : {&in, &dog, &taps, &mm, &tmp_a, &tmp_b, &tmp_c, &tmp_d}) b->release();
         g12.release();
         keys.release(); keys_sorted.release(); vals.release(); vals_sorted.release();
         recs.release(); peaks.release(); count.release(); sort_tmp.release();
+        loc.release(); ips.release(); ips_sel.release(); flags.release(); sel_tmp.release(); nsel.release();
     }
 };
 
@@ -1293,7 +1301,33 @@ void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p
     }
 }
 
-// ProcessDOG.compute's result: interest points after Localization (:150-168)
+// candidates -> interest points on the device: Localization.noLocalization (:19-45)
+// copies them; with quadratic localisation (:47-88) the caller keeps those whose fitted
+// |value| > threshold (flag), in candidate order
+template <bool LOC>
+__global__ void k_to_points(const PeakOut* __restrict__ pk, const LocOut* __restrict__ loc, int64_t np, float thr,
+                            spim_interest_point* __restrict__ ips, unsigned char* __restrict__ flags) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    spim_interest_point ip{};
+    if constexpr (LOC) {
+        const LocOut l = loc[i];
+        for (int a = 0; a < 3; ++a) ip.pos[a] = l.pos[a];
+        ip.intensity = l.value;
+        flags[i] = fabsf(l.value) > thr ? 1 : 0;   // float against float (Localization.java:74)
+    } else {
+        ip.pos[0] = pk[i].x;
+        ip.pos[1] = pk[i].y;
+        ip.pos[2] = pk[i].z;
+        ip.intensity = pk[i].intensity;
+    }
+    ip.is_max = pk[i].is_max;
+    ips[i] = ip;
+}
+
+// ProcessDOG.compute's result: interest points after Localization (:150-168).  The
+// candidates (threshold / 10 with quadratic localisation: millions on a noisy 768^3
+// view) stay on the device; only the interest points are copied out.
 void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_params* p, float* dog_out,
                          spim_interest_point* out, int64_t max_out, int64_t* nout) {
     SD_CHECK(nout && p, SPIMDECON_ERR_ARG, "null argument");
@@ -1305,40 +1339,41 @@ void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_p
     DogRun r;
     dog_run(img, dims, p, dog_out, p->localization == 1 || dog_out != nullptr, sh.s, w, r);
     const int64_t np = r.np;
-    std::vector<PeakOut> hp(np);
-    if (np > 0) SD_HIP(hipMemcpyAsync(hp.data(), r.dpeaks, np * sizeof(PeakOut), hipMemcpyDeviceToHost, sh.s));
-    std::vector<spim_interest_point> pts;
-    if (p->localization == 0) {  // Localization.noLocalization (:19-45)
-        SD_HIP(hipStreamSynchronize(sh.s));
-        pts.resize(np);
-        for (int64_t i = 0; i < np; ++i) {
-            pts[i].pos[0] = hp[i].x;
-            pts[i].pos[1] = hp[i].y;
-            pts[i].pos[2] = hp[i].z;
-            pts[i].intensity = hp[i].intensity;
-            pts[i].is_max = hp[i].is_max;
+    int64_t n = 0;
+    const spim_interest_point* res = nullptr;
+    if (np > 0) {
+        grow(w.ips, size_t(np));
+        const unsigned grid = unsigned(ceil_div(np, int64_t(256)));
+        if (p->localization == 0) {
+            hipLaunchKernelGGL(k_to_points<false>, dim3(grid), dim3(256), 0, sh.s, r.dpeaks, nullptr, np, 0.0f,
+                               w.ips.p, nullptr);
+            SD_HIP(hipGetLastError());
+            res = w.ips.p;
+            n = np;
+        } else {
+            grow(w.loc, size_t(np));
+            grow(w.flags, size_t(np));
+            grow(w.ips_sel, size_t(np));
+            grow(w.nsel, 1);
+            hipLaunchKernelGGL(k_localize, dim3(grid), dim3(256), 0, sh.s, r.dog, r.d, r.dpeaks, np, w.loc.p);
+            SD_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_to_points<true>, dim3(grid), dim3(256), 0, sh.s, r.dpeaks, w.loc.p, np,
+                               float(p->threshold), w.ips.p, w.flags.p);
+            SD_HIP(hipGetLastError());
+            const size_t tb = point_select_temp_bytes(np);
+            grow(w.sel_tmp, std::max<size_t>(tb, 1));
+            point_select(w.sel_tmp.p, tb, w.ips.p, w.flags.p, w.ips_sel.p, w.nsel.p, np, sh.s);
+            int hn = 0;
+            SD_HIP(hipMemcpyAsync(&hn, w.nsel.p, sizeof(int), hipMemcpyDeviceToHost, sh.s));
+            SD_HIP(hipStreamSynchronize(sh.s));
+            res = w.ips_sel.p;
+            n = hn;
         }
-    } else if (np > 0) {  // Localization.computeQuadraticLocalization (:47-88)
-        DBuf<LocOut> dloc(np);
-        hipLaunchKernelGGL(k_localize, dim3(unsigned(ceil_div(np, 256))), dim3(256), 0, sh.s, r.dog, r.d,
-                           r.dpeaks, np, dloc.p);
-        SD_HIP(hipGetLastError());
-        std::vector<LocOut> loc(np);
-        SD_HIP(hipMemcpyAsync(loc.data(), dloc.p, np * sizeof(LocOut), hipMemcpyDeviceToHost, sh.s));
-        SD_HIP(hipStreamSynchronize(sh.s));
-        for (int64_t i = 0; i < np; ++i) {
-            if (!(std::fabs(loc[i].value) > p->threshold)) continue;
-            spim_interest_point ip{};
-            for (int a = 0; a < 3; ++a) ip.pos[a] = loc[i].pos[a];
-            ip.intensity = loc[i].value;
-            ip.is_max = hp[i].is_max;
-            pts.push_back(ip);
-        }
-    } else {
-        SD_HIP(hipStreamSynchronize(sh.s));
     }
-    *nout = int64_t(pts.size());
-    if (out) std::copy(pts.begin(), pts.begin() + std::min<int64_t>(max_out, int64_t(pts.size())), out);
+    const int64_t m = out ? std::min<int64_t>(max_out, n) : 0;
+    if (m > 0) SD_HIP(hipMemcpyAsync(out, res, size_t(m) * sizeof(spim_interest_point), hipMemcpyDefault, sh.s));
+    SD_HIP(hipStreamSynchronize(sh.s));
+    *nout = n;
 }
 
 void dog_release_workspace(int dev) {

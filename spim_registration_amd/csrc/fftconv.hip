@@ -946,6 +946,35 @@ static int zdma_tx(int64_t Mz, int cz) {
     return 0;
 }
 
+// k_zdmc: z chunks carried inside a block.  Tile width TX = 32 columns (256-B plane
+// segments) when its two buffers fit, else 16; OPT outputs per thread from the
+// instantiated set with the fewest idle output slots (nch * TR * OPT - nz), chunks of
+// H = ceil(nz / nch).  SPIMDECON_ZCHUNK=0 keeps k_zdma, =16 / =32 forces the width.
+struct ZChunk { int tx = 0, opt = 0, H = 0; };
+static ZChunk zdmc_plan(int64_t nz, int KC) {
+    const char* e = std::getenv("SPIMDECON_ZCHUNK");
+    const int force = e ? std::atoi(e) : -1;
+    ZChunk best;
+    if (force == 0 || KC == 0 || nz < 1) return best;
+    struct Cand { int tx, opt; };
+    std::vector<Cand> cands;
+    if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
+    else cands = {{32, 16}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
+    int64_t bw = -1;
+    for (const Cand& c : cands) {
+        if (force > 0 && c.tx != force) continue;
+        if (best.tx != 0 && c.tx < best.tx) break;   // the widest tile that fits wins
+        const int64_t cap = int64_t(kZdThreads / c.tx) * c.opt;
+        const int64_t nch = ceil_div(nz, cap);
+        const int64_t waste = nch * cap - nz;
+        if (bw < 0 || waste < bw) {
+            best = {c.tx, c.opt, int(ceil_div(nz, nch))};
+            bw = waste;
+        }
+    }
+    return best;
+}
+
 static size_t zdirect_lds(const SpectralPlan& p, int KC) {
     return size_t((p.g.Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
 }
@@ -966,10 +995,39 @@ bool engine_zdirect_ok(const SpectralPlan& p) {
 
 int engine_zpass_mode(const SpectralPlan& p, bool compact) {
     if (!compact) return 0;
-    return engine_zdirect_ok(p) ? 2 : 1;
+    if (!engine_zdirect_ok(p)) return 1;
+    return (p.g.My * p.Hp) % 16 == 0 && zdmc_plan(p.g.nz, zdirect_kc_bound(p.g.cz)).tx > 0 ? 3 : 2;
 }
 
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
+    const int64_t nflat = p.g.My * p.Hp;
+    if (engine_zdirect_ok(p) && nflat % 16 == 0 && zdmc_plan(p.g.nz, zdirect_kc_bound(p.g.cz)).tx > 0) {
+        const int KC = zdirect_kc_bound(p.g.cz);
+        const ZChunk zc = zdmc_plan(p.g.nz, KC);
+        const int64_t ntiles = ceil_div(nflat, int64_t(zc.tx));
+        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256));
+        const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
+        const float kscale = float(p.g.Mz);
+        bool done = false;
+#define SD_ZC(KCV, OPTV, TXV)                                                                           \
+        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV)) {                               \
+            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV));                                         \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV>),          \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
+            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, C, \
+                               Kc, p.g.cz, zc.H, bytes, kscale);                                        \
+            done = true;                                                                                \
+        }
+#define SD_ZC4(KCV) SD_ZC(KCV, 16, 32) SD_ZC(KCV, 12, 32) SD_ZC(KCV, 8, 32) SD_ZC(KCV, 17, 16) \
+        SD_ZC(KCV, 13, 16) SD_ZC(KCV, 9, 16)
+        SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
+        SD_ZC(16, 15, 32) SD_ZC(16, 12, 32) SD_ZC(16, 8, 32) SD_ZC(16, 17, 16) SD_ZC(16, 13, 16) SD_ZC(16, 9, 16)
+#undef SD_ZC4
+#undef SD_ZC
+        SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");
+        SD_HIP(hipGetLastError());
+        return;
+    }
     if (engine_zdirect_ok(p) && zdma_tx(p.g.Mz, p.g.cz) > 0 && p.Hp % 16 == 0) {
         const int KC = zdirect_kc_bound(p.g.cz);
         const int tx = zdma_tx(p.g.Mz, p.g.cz);

@@ -71,6 +71,22 @@ def test_dog_quadratic_localization(gpu, find_min, find_max):
     assert np.any(np.abs(got - np.round(got)) > 1e-3)      # genuinely sub-pixel
 
 
+def test_dog_localized_threshold_is_a_float(gpu):
+    """ProcessDOG takes a float threshold and Localization keeps |fitted value| >
+    threshold in float (Localization.java:47,74): a double threshold just below a
+    fitted value, which rounds to that value as a float, drops the point."""
+    img = bead_stack(cid=13)
+    pts = dog.compute(img, sigma=1.8, threshold=0.008, localization=1, keep_intensity=True)
+    v = np.float32(abs(pts[len(pts) // 2].intensity))
+    thr = float(v) - float(np.spacing(v)) / 4          # < v as a double, == v as a float
+    assert np.float32(thr) == v and thr < float(v)
+    got = dog.compute(img, sigma=1.8, threshold=thr, localization=1, keep_intensity=True)
+    exp, _ = dog_ref.process_dog(img, 1.8, thr, localization=1)
+    assert len(got) == len(exp)
+    assert not any(np.float32(abs(p.intensity)) == v for p in got)
+    np.testing.assert_allclose([p.location for p in got], [e[:3] for e in exp], rtol=0, atol=1e-5)
+
+
 def test_dog_simple_peaks_threshold_tenth(gpu):
     """getSimplePeaks at localization 1 uses threshold / 10 (ProcessDOG.java:63-67)."""
     img = bead_stack(shape=(24, 26, 30), cid=14)
