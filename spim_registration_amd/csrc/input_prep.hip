@@ -65,10 +65,9 @@ __global__ __launch_bounds__(kIpBlock) void k_transform_view(ViewArgs v, int64_t
                                                              const double* __restrict__ lut,
                                                              float* __restrict__ img_out,
                                                              float* __restrict__ w_out) {
-    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
-    if (i >= n) return;
     int64_t x, y, z;
-    flat_xyz(i, nx, ny, n, x, y, z);
+    if (!tiled_xyz(nx, ny, n / (nx * ny), x, y, z)) return;
+    const int64_t i = (z * ny + y) * nx + x;
     // TransformInput: s = (float) position + offset; t = inv3 (s - translation)
     const float s0 = float(x) + float(bx), s1 = float(y) + float(by), s2 = float(z) + float(bz);
     const double d0 = double(s0) - v.a.tr[0], d1 = double(s1) - v.a.tr[1], d2 = double(s2) - v.a.tr[2];
@@ -183,10 +182,9 @@ __global__ __launch_bounds__(kIpBlock) void k_fuse(const FuseView* __restrict__ 
                                                    int64_t by, int64_t bz, int64_t nx, int64_t ny, int64_t n,
                                                    float ds, int interp, int blend, const double* __restrict__ lut,
                                                    float* __restrict__ out) {
-    const int64_t i = int64_t(blockIdx.x) * kIpBlock + threadIdx.x;
-    if (i >= n) return;
     int64_t x, y, z;
-    flat_xyz(i, nx, ny, n, x, y, z);
+    if (!tiled_xyz(nx, ny, n / (nx * ny), x, y, z)) return;
+    const int64_t i = (z * ny + y) * nx + x;
     float f0 = float(x), f1 = float(y), f2 = float(z);
     if (ds != 1.0f) {
         f0 = f0 * ds;
@@ -290,7 +288,9 @@ void prepare_inputs(int nviews, const spim_view_source* views, const spim_input_
             a.border[d] = p->blending_border[d];
             a.range[d] = p->blending_range[d];
         }
-        hipLaunchKernelGGL(k_transform_view, dim3(grid), dim3(kIpBlock), 0, s, a, p->bb_min[0], p->bb_min[1],
+        SD_CHECK(tiled_blocks(nx, ny, nz) < (int64_t(1) << 31), SPIMDECON_ERR_ARG, "bounding box too large");
+        hipLaunchKernelGGL(k_transform_view, dim3(unsigned(tiled_blocks(nx, ny, n / (nx * ny)))), dim3(kIpBlock), 0,
+                           s, a, p->bb_min[0], p->bb_min[1],
                            p->bb_min[2], nx, ny, n, p->weight_type, dlut.p, dimg[v], dw[v]);
         SD_HIP(hipGetLastError());
         SD_HIP(hipStreamSynchronize(s));  // the source buffer is released at the end of the iteration
@@ -400,7 +400,9 @@ void fuse_weighted_average(int nviews, const spim_view_source* views, const spim
         dout.alloc(n);
         o = dout.p;
     }
-    hipLaunchKernelGGL(k_fuse, dim3(unsigned(ceil_div(n, int64_t(kIpBlock)))), dim3(kIpBlock), 0, s, dfv.p,
+    static_assert(kIpBlock == kTileX * kTileZ, "one tile per block");
+    SD_CHECK(tiled_blocks(nx, ny, nz) < (int64_t(1) << 31), SPIMDECON_ERR_ARG, "bounding box too large");
+    hipLaunchKernelGGL(k_fuse, dim3(unsigned(tiled_blocks(nx, ny, n / (nx * ny)))), dim3(kIpBlock), 0, s, dfv.p,
                        nviews, p->bb_min[0], p->bb_min[1], p->bb_min[2], nx, ny, n, p->downsampling,
                        p->interpolation, p->use_blending ? 1 : 0, dlut.p, o);
     SD_HIP(hipGetLastError());

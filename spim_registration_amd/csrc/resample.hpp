@@ -85,6 +85,25 @@ __device__ float nlinear_at(const float* src, int sx, int sy, int sz, double p0,
 
 // (x, y, z) of a flat x-fastest index: 32-bit divisions when the volume allows
 // (a 64-bit division is a ~100-instruction software routine on the GPU)
+// Output traversal in (x, z) tiles of kTileX x kTileZ voxels, one y row each, y fastest
+// over the blocks: the voxels of a block then sample a compact source region (a rotated
+// view's x runs cross the source's z planes diagonally: a 256-voxel x run touched ~180
+// 2.4-MB planes, a 32 x 8 tile ~30) while each block still writes whole 128-B row
+// segments.  Per-voxel arithmetic is unchanged (bit-identical output).
+constexpr int kTileX = 32, kTileZ = 8;
+inline int64_t tiled_blocks(int64_t nx, int64_t ny, int64_t nz) {
+    return ny * ((nx + kTileX - 1) / kTileX) * ((nz + kTileZ - 1) / kTileZ);
+}
+__device__ __forceinline__ bool tiled_xyz(int64_t nx, int64_t ny, int64_t nz, int64_t& x, int64_t& y, int64_t& z) {
+    const int64_t b = blockIdx.x;
+    const int64_t ntx = (nx + kTileX - 1) / kTileX;
+    y = b % ny;
+    const int64_t r = b / ny;
+    x = (r % ntx) * kTileX + threadIdx.x % kTileX;
+    z = (r / ntx) * kTileZ + threadIdx.x / kTileX;
+    return x < nx && z < nz;
+}
+
 __device__ __forceinline__ void flat_xyz(int64_t i, int64_t nx, int64_t ny, int64_t n, int64_t& x, int64_t& y,
                                          int64_t& z) {
     if (n < (int64_t(1) << 32)) {
