@@ -97,7 +97,7 @@ def pmc_traffic(cls, M, args):
     if cls == "z_convolve":
         hits = hits[:1]
     return (int(sum(b for _, b in hits) / len(hits)),
-            f"{d['file']}: " + " / ".join(n for n, _ in hits) + (" (mean)" if len(hits) > 1 else ""))
+            "profiles/pmc_traffic.json: " + " / ".join(n for n, _ in hits) + (" (mean)" if len(hits) > 1 else ""))
 
 
 def cpu_model():
