@@ -414,6 +414,18 @@ int spim_extract_psf(const float* img, const int64_t dims[3], int img_on_device,
                      int64_t nlocations, const int64_t psf_size[3], const double model[12], float* psf_original,
                      float* psf_transformed, int device);
 
+/* spim_extract_psf for nviews views at once (ExtractPSF.extract over the views of a
+ * timepoint): dims, models are nviews x 3 / x 12 (models may be NULL when
+ * psf_transformed is NULL; entries of psf_transformed may be NULL); psf_original
+ * and psf_transformed entries may be host or device pointers.  The views run
+ * concurrently on their own streams: one view's bead sum is psf_size serial float
+ * chains (bead order, as the reference), too few to fill the GPU alone.  Results are
+ * identical to nviews spim_extract_psf calls. */
+int spim_extract_psfs(int nviews, const float* const* imgs, const int64_t* dims, int img_on_device,
+                      const double* const* locations, const int64_t* nlocations, const int64_t psf_size[3],
+                      const double* models, float* const* psf_original, float* const* psf_transformed,
+                      int device);
+
 /* computeAverageTransformedPSF (:164-208): the PSFs (psf_dims = npsfs x 3)
  * point-mirrored about their centres and summed into the max size, written
  * to avg_dims.  avg == NULL: only the dims are returned. */

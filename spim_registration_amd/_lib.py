@@ -145,6 +145,8 @@ SIGNATURES = {
     "spim_psf_transformed_size": (C.c_int, [_pi64, _pd, _pi64, _pd]),
     "spim_transform_psf": (C.c_int, [_pf, _pi64, _pd, _pf, C.c_int]),
     "spim_extract_psf": (C.c_int, [C.c_void_p, _pi64, C.c_int, _pd, C.c_int64, _pi64, _pd, _pf, _pf, C.c_int]),
+    "spim_extract_psfs": (C.c_int, [C.c_int, C.POINTER(C.c_void_p), _pi64, C.c_int, C.POINTER(C.c_void_p), _pi64,
+                                    _pi64, _pd, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int]),
     "spim_average_transformed_psf": (C.c_int, [C.c_int, C.POINTER(_pf), _pi64, _pf, _pi64, C.c_int]),
     "spim_max_projection": (C.c_int, [_pf, _pi64, C.c_int, _pf, _pi64, C.POINTER(C.c_int), C.c_int]),
     "spim_fuse_weighted_average": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(FusionParams),

@@ -16,6 +16,8 @@
 #include <cmath>
 #include <vector>
 
+#include <memory>
+
 #include "common.hpp"
 #include "resample.hpp"
 #include "spimdecon.h"
@@ -249,59 +251,110 @@ void transform_psf(const float* psf, const int64_t* psf_size, const double* mode
     SD_HIP(hipStreamSynchronize(st.s));
 }
 
+// One view's ExtractPSF.extract (:281-299) + transformPSF, in three steps so several
+// views can run concurrently (extract_psfs): the per-voxel sum over the beads is a
+// serial float chain in bead order (bit-exact with the reference), so one view offers
+// only psf_size (~9k) parallel chains; eight views on eight streams fill 8x more.
+struct PsfJob {
+    const float* img = nullptr;
+    Dim3 s{}, p{};
+    const double* model = nullptr;
+    int64_t nloc = 0;
+    float* psf_original = nullptr;
+    float* psf_transformed = nullptr;
+    int64_t psf_size[3] = {0, 0, 0};
+    Stream st;
+    DBuf<float> dimg, dpsf, samp, dt;
+    DBuf<double> dloc, mm;
+    const float* src = nullptr;
+    int64_t chunk = 0;
+
+    PsfJob(const float* img_, const int64_t* dims, int img_on_device, const double* locations, int64_t nloc_,
+           const int64_t* psf_size_, const double* model_, float* orig, float* trans)
+        : img(img_), model(model_), nloc(nloc_), psf_original(orig), psf_transformed(trans) {
+        SD_CHECK(img && psf_original && nloc >= 0 && (nloc == 0 || locations), SPIMDECON_ERR_ARG, "null argument");
+        SD_CHECK(!psf_transformed || model, SPIMDECON_ERR_ARG, "a transformed PSF needs the view model");
+        s = dim3_of(dims, "image");
+        p = dim3_of(psf_size_, "psf");
+        std::memcpy(psf_size, psf_size_, sizeof(psf_size));
+        // allocations and uploads (asynchronous on this job's stream)
+        src = img;
+        if (!img_on_device) {
+            dimg.alloc(s.n());
+            SD_HIP(hipMemcpyAsync(dimg.p, img, s.n() * 4, hipMemcpyHostToDevice, st.s));
+            src = dimg.p;
+        }
+        dloc.alloc(size_t(std::max<int64_t>(nloc, 1)) * 3);
+        if (nloc) SD_HIP(hipMemcpyAsync(dloc.p, locations, nloc * 24, hipMemcpyHostToDevice, st.s));
+        dpsf.alloc(p.n());
+        mm.alloc(2);
+        if (nloc > 64) {   // bead chunks of <= 2^26 samples (256 MB)
+            chunk = std::max<int64_t>(1, std::min<int64_t>(nloc, (int64_t(1) << 26) / p.n()));
+            samp.alloc(size_t(chunk * p.n()));
+        }
+        if (psf_transformed) {
+            int64_t ts[3];
+            double off[3];
+            transformed_size(psf_size, model, ts, off);
+            dt.alloc(dim3_of(ts, "transformed psf").n());
+        }
+    }
+
+    void launch() {
+        if (nloc <= 64) {
+            hipLaunchKernelGGL(k_psf_extract, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, src, s, dloc.p, nloc,
+                               p, dpsf.p);
+        } else {
+            SD_HIP(hipMemsetAsync(dpsf.p, 0, p.n() * 4, st.s));
+            for (int64_t l0 = 0; l0 < nloc; l0 += chunk) {
+                const int64_t nb = std::min(chunk, nloc - l0);
+                hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(nb * p.n(), kPsfBlock))), dim3(kPsfBlock),
+                                   0, st.s, src, s, dloc.p + 3 * l0, nb, p, samp.p);
+                hipLaunchKernelGGL(k_psf_accumulate, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, samp.p, nb,
+                                   p.n(), dpsf.p);
+            }
+        }
+        SD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_psf_minmax, dim3(1), dim3(1024), 0, st.s, dpsf.p, p.n(), mm.p);
+        SD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, dpsf.p, p.n(), mm.p);
+        SD_HIP(hipGetLastError());
+        SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDefault, st.s));
+        if (psf_transformed) {
+            Dim3 t;
+            launch_transform(dpsf.p, p, model, dt.p, t, st.s);
+            SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, t.n() * 4, hipMemcpyDefault, st.s));
+        }
+    }
+
+    void finish() { SD_HIP(hipStreamSynchronize(st.s)); }
+};
+
 void extract_psf(const float* img, const int64_t* dims, int img_on_device, const double* locations, int64_t nloc,
                  const int64_t* psf_size, const double* model, float* psf_original, float* psf_transformed,
                  int device) {
-    SD_CHECK(img && psf_original && nloc >= 0 && (nloc == 0 || locations), SPIMDECON_ERR_ARG, "null argument");
-    SD_CHECK(!psf_transformed || model, SPIMDECON_ERR_ARG, "a transformed PSF needs the view model");
-    const Dim3 s = dim3_of(dims, "image");
-    const Dim3 p = dim3_of(psf_size, "psf");
     check_device(device);
     DeviceGuard guard(device);
-    Stream st;
-    DBuf<float> dimg;
-    const float* src = img;
-    if (!img_on_device) {
-        dimg.alloc(s.n());
-        SD_HIP(hipMemcpyAsync(dimg.p, img, s.n() * 4, hipMemcpyHostToDevice, st.s));
-        src = dimg.p;
-    }
-    DBuf<double> dloc(size_t(std::max<int64_t>(nloc, 1)) * 3);
-    if (nloc) SD_HIP(hipMemcpyAsync(dloc.p, locations, nloc * 24, hipMemcpyHostToDevice, st.s));
-    DBuf<float> dpsf(p.n());
-    DBuf<double> mm(2);
-    if (nloc <= 64) {
-        hipLaunchKernelGGL(k_psf_extract, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, src, s, dloc.p, nloc, p,
-                           dpsf.p);
-    } else {   // bead chunks of <= 2^26 samples (256 MB)
-        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nloc, (int64_t(1) << 26) / p.n()));
-        DBuf<float> samp(size_t(chunk * p.n()));
-        SD_HIP(hipMemsetAsync(dpsf.p, 0, p.n() * 4, st.s));
-        for (int64_t l0 = 0; l0 < nloc; l0 += chunk) {
-            const int64_t nb = std::min(chunk, nloc - l0);
-            hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(nb * p.n(), kPsfBlock))), dim3(kPsfBlock), 0,
-                               st.s, src, s, dloc.p + 3 * l0, nb, p, samp.p);
-            hipLaunchKernelGGL(k_psf_accumulate, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, samp.p, nb, p.n(),
-                               dpsf.p);
-        }
-    }
-    SD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_psf_minmax, dim3(1), dim3(1024), 0, st.s, dpsf.p, p.n(), mm.p);
-    SD_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, dpsf.p, p.n(), mm.p);
-    SD_HIP(hipGetLastError());
-    SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDeviceToHost, st.s));
-    DBuf<float> dt;
-    if (psf_transformed) {
-        int64_t ts[3];
-        double off[3];
-        transformed_size(psf_size, model, ts, off);
-        dt.alloc(dim3_of(ts, "transformed psf").n());
-        Dim3 t;
-        launch_transform(dpsf.p, p, model, dt.p, t, st.s);
-        SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, t.n() * 4, hipMemcpyDeviceToHost, st.s));
-    }
-    SD_HIP(hipStreamSynchronize(st.s));
+    PsfJob job(img, dims, img_on_device, locations, nloc, psf_size, model, psf_original, psf_transformed);
+    job.launch();
+    job.finish();
+}
+
+void extract_psfs(int nviews, const float* const* imgs, const int64_t* dims, int img_on_device,
+                  const double* const* locations, const int64_t* nlocations, const int64_t* psf_size,
+                  const double* models, float* const* psf_original, float* const* psf_transformed, int device) {
+    SD_CHECK(nviews >= 0 && (nviews == 0 || (imgs && dims && locations && nlocations && psf_original)),
+             SPIMDECON_ERR_ARG, "null argument");
+    check_device(device);
+    DeviceGuard guard(device);
+    std::vector<std::unique_ptr<PsfJob>> jobs;
+    jobs.reserve(size_t(nviews));
+    for (int v = 0; v < nviews; ++v)
+        jobs.emplace_back(new PsfJob(imgs[v], dims + 3 * v, img_on_device, locations[v], nlocations[v], psf_size,
+                                     models ? models + 12 * v : nullptr, psf_original[v],
+                                     psf_transformed ? psf_transformed[v] : nullptr));
+    for (auto& j : jobs) j->launch();
+    for (auto& j : jobs) j->finish();
 }
 
 void average_transformed_psf(int npsf, const float* const* psfs, const int64_t* psf_dims, float* avg,
@@ -387,6 +440,16 @@ extern "C" int spim_extract_psf(const float* img, const int64_t dims[3], int img
     return guarded([&] {
         extract_psf(img, dims, img_on_device, locations, nlocations, psf_size, model, psf_original, psf_transformed,
                     device);
+    });
+}
+
+extern "C" int spim_extract_psfs(int nviews, const float* const* imgs, const int64_t* dims, int img_on_device,
+                                 const double* const* locations, const int64_t* nlocations,
+                                 const int64_t psf_size[3], const double* models, float* const* psf_original,
+                                 float* const* psf_transformed, int device) {
+    return guarded([&] {
+        extract_psfs(nviews, imgs, dims, img_on_device, locations, nlocations, psf_size, models, psf_original,
+                     psf_transformed, device);
     });
 }
 

@@ -124,12 +124,11 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     imgs, ws, info = input_prep.prepare_inputs(views, models, bb_min, bb_dims, blending_border, blending_range,
                                                weight_type, device=device)   # 3a.
     t = lap("prepare_inputs", t)
-    psfs = []
-    for v, m, p, c in zip(views, models, points, corr):       # 3b. ExtractPSF from corresponding beads
-        # (a view with no corresponding bead -- registration would have failed for it --
-        # takes all of its detections rather than an all-zero PSF)
-        _, tr = psf_mod.extract_psf(v, p[c] if len(c) else p, psf_size, m, device=device)
-        psfs.append(tr)
+    # 3b. ExtractPSF from the corresponding beads, all views at once (a view with no
+    # corresponding bead -- registration would have failed for it -- takes all of its
+    # detections rather than an all-zero PSF)
+    beads = [p[c] if len(c) else p for p, c in zip(points, corr)]
+    psfs = [tr for _, tr in psf_mod.extract_psfs(list(views), beads, psf_size, list(models), device=device)]
     t = lap("extract_psf", t)
     shape = tuple(imgs[0].shape)
     sess = Session((shape[2], shape[1], shape[0]), device=device)            # 4. MVDeconvolution

@@ -70,6 +70,47 @@ def extract_psf(img, locations, psf_size, model=None, device: int = 0):
     return orig, trans
 
 
+def extract_psfs(imgs, locations, psf_size, models=None, device: int = 0):
+    """extract_psf for the views of a timepoint in one call (ExtractPSF.extract over
+    the views): the views run concurrently on the GPU; results are identical to
+    per-view extract_psf calls.  imgs: torch tensors on the GPU (all of them) or
+    numpy arrays; models: per view, or None."""
+    lib = _lib.load()
+    n = len(imgs)
+    on_dev = 1 if n and hasattr(imgs[0], "is_cuda") and imgs[0].is_cuda else 0
+    keep, ptrs, dims = [], [], []
+    for im in imgs:
+        if on_dev:
+            if not (hasattr(im, "is_cuda") and im.is_cuda):
+                raise ValueError("imgs must be all GPU tensors or all host arrays")
+            im = im.contiguous().float()
+            ptrs.append(im.data_ptr())
+        else:
+            im = np.ascontiguousarray(im, np.float32)
+            ptrs.append(im.ctypes.data)
+        keep.append(im)
+        dims += [im.shape[2], im.shape[1], im.shape[0]]
+    locs = [np.ascontiguousarray(np.asarray(l, np.float64).reshape(-1, 3)) for l in locations]
+    size = [int(v) for v in psf_size]
+    origs = [np.empty((size[2], size[1], size[0]), np.float32) for _ in range(n)]
+    trans = None
+    if models is not None:
+        trans = []
+        for m in models:
+            (tx, ty, tz), _ = transformed_size(size, m)
+            trans.append(np.empty((tz, ty, tx), np.float32))
+    vp = C.c_void_p * max(n, 1)
+    check(lib.spim_extract_psfs(n, vp(*ptrs), (C.c_int64 * max(3 * n, 1))(*dims), on_dev,
+                                vp(*[l.ctypes.data if len(l) else None for l in locs]),
+                                (C.c_int64 * max(n, 1))(*[len(l) for l in locs]), (C.c_int64 * 3)(*size),
+                                (C.c_double * (12 * n))(*[float(v) for m in models
+                                                          for v in np.asarray(m, np.float64).reshape(12)])
+                                if models is not None else None,
+                                vp(*[o.ctypes.data for o in origs]),
+                                vp(*[t.ctypes.data for t in trans]) if trans is not None else None, device))
+    return [(origs[v], trans[v] if trans is not None else None) for v in range(n)]
+
+
 def average_transformed_psf(psfs, device: int = 0) -> np.ndarray:
     """ExtractPSF.computeAverageTransformedPSF (:164-208)."""
     lib = _lib.load()

@@ -86,3 +86,26 @@ def test_extract_psf_many_beads_two_phase(gpu, nbeads):
     np.testing.assert_allclose(orig, eo, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(trans, et, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(few, pr.extract_next_img(img, ROT, locs[:64], (9, 9, 11))[0], rtol=1e-6, atol=1e-7)
+
+
+def test_extract_psfs_batch_equals_per_view(gpu):
+    """spim_extract_psfs: several views (device tensors, few and many beads, one view
+    without beads) at once give the bits of per-view spim_extract_psf calls."""
+    views, beads, models = [], [], []
+    rng = np.random.default_rng(5)
+    for v, nb in enumerate([12, 0, 300, 70]):
+        img, locs = bead_view(cid=30 + v)
+        if nb != 12:
+            locs = rng.uniform([0, 0, 0], [64, 56, 40], size=(nb, 3))
+        views.append(torch.from_numpy(img).cuda())
+        beads.append(locs)
+        models.append(ROT if v % 2 == 0 else np.hstack([np.eye(3), np.zeros((3, 1))]))
+    got = psf.extract_psfs(views, beads, (9, 9, 11), models)
+    for v in range(4):
+        o, t = psf.extract_psf(views[v], beads[v], (9, 9, 11), models[v])
+        np.testing.assert_array_equal(got[v][0], o)
+        np.testing.assert_array_equal(got[v][1], t)
+    host = psf.extract_psfs([x.cpu().numpy() for x in views], beads, (9, 9, 11), None)
+    for v in range(4):
+        np.testing.assert_array_equal(host[v][0], got[v][0])
+        assert host[v][1] is None
