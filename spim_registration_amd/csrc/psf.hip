@@ -319,15 +319,19 @@ struct PsfJob {
         SD_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, dpsf.p, p.n(), mm.p);
         SD_HIP(hipGetLastError());
-        SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDefault, st.s));
         if (psf_transformed) {
             Dim3 t;
             launch_transform(dpsf.p, p, model, dt.p, t, st.s);
-            SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, t.n() * 4, hipMemcpyDefault, st.s));
         }
     }
 
-    void finish() { SD_HIP(hipStreamSynchronize(st.s)); }
+    // the copies out only now: a copy into pageable host memory blocks the host until
+    // the stream has drained, which would serialise the views' launches
+    void finish() {
+        SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDefault, st.s));
+        if (psf_transformed) SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, dt.n * 4, hipMemcpyDefault, st.s));
+        SD_HIP(hipStreamSynchronize(st.s));
+    }
 };
 
 void extract_psf(const float* img, const int64_t* dims, int img_on_device, const double* locations, int64_t nloc,
