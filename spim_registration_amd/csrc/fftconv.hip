@@ -660,12 +660,18 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // modes: planes stored) -- the RL loop only reads the nz interior planes back
     if (nout < 0) nout = int(p.g.Mz);
     const int L = f.L;
-    // 16-column tiles (128-B row segments) when they fit the LDS budget of the factor
-    // pair's occupancy (80 KB at 32 threads per column, 160 KB at 64); else 8 columns
+    // 16-column tiles (128-B row segments) when they fit the LDS (160 KB); else 8 columns
     // (8-column tiles measured slower for the fused z pass, 0.69 vs 0.60 ms, but beat
     // the Stockham passes: L = 640 / 800 / 1024 at 32 threads, 2100 at 64)
     const int tr = (f.n1 > 32 || f.n2 > 32) ? 64 : 32;  // SD_2F_TR
-    const size_t budget = size_t(tr == 64 ? 160 : 80) * 1024;
+    // 16-column tiles up to 160 KB (one block per CU) rather than 8-column tiles at two
+    // blocks per CU: 128-B segments won at 800 (C4 RL 815 -> 745 ms per timepoint);
+    // SPIMDECON_COL_WIDE=0 restores the 80-KB budget
+    static const bool wide = [] {
+        const char* e = std::getenv("SPIMDECON_COL_WIDE");
+        return !(e && e[0] == '0');
+    }();
+    const size_t budget = size_t(tr == 64 || wide ? 160 : 80) * 1024;
     auto tile_lds = [&](int tx) { return size_t(L * tx + L + (MODE == 5 ? f.n2 * tx : 0)) * sizeof(float2); };
     const int TX = tile_lds(k2fTX) <= budget ? k2fTX : 8;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
