@@ -131,15 +131,19 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     psfs = [tr for _, tr in psf_mod.extract_psfs(list(views), beads, psf_size, list(models), device=device)]
     t = lap("extract_psf", t)
     shape = tuple(imgs[0].shape)
+    t_setup = t
     sess = Session((shape[2], shape[1], shape[0]), device=device)            # 4. MVDeconvolution
     try:
+        t = lap("rl_setup_create", t)
         for i, w, k in zip(imgs, ws, psfs):
             sess.add_view_device(i.data_ptr(), w.data_ptr(), k)
+        t = lap("rl_setup_add_views", t)
         sess.init(psftype)
         sess.init_psi()
         engine = {"fft_dims_xyz": list(sess.fft_dims(0)), "zpass_mode": sess.zpass_mode(0),
                   "kernel_planes": sess.kernel_planes(0)}
-        t = lap("rl_setup", t)
+        t = lap("rl_setup_init", t)
+        ms["rl_setup"] = round((t - t_setup) * 1e3, 2)
         stats = sess.run(iterations, lam)
         engine["xpass_mode"] = sess.xpass_mode(0)
         sess.apply_mask()
