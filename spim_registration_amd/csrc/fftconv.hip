@@ -533,7 +533,7 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     XArgs b;
     if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
-    const size_t lds = size_t(L + 2 + np * xt_pitch(L)) * sizeof(float2);
+    const size_t lds = xt_lds(L, np, xt_twg(L, np));
     if (lds > 160 * 1024) return 0;
     const int64_t ntiles = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, np));
     // blocks: one tile each by default (SPIMDECON_XGRID=N caps the grid at N resident-

@@ -323,6 +323,31 @@ def test_long_columns_on_8_column_tiles(gpu, shape, ksize, env, zmode, monkeypat
     assert rel_l2(out[0], res.psi) < TOL
 
 
+@pytest.mark.parametrize("shape,lx", [((6, 10, 360), 384), ((6, 10, 552), 576), ((5, 9, 776), 800)])
+def test_x_tiles_with_global_twiddles(gpu, shape, lx):
+    """Row lengths whose x tiles fit one more block per CU without the LDS twiddle
+    table (384, 576, 800: xt_twg) read the phase-A twiddles from global memory;
+    the tile path must still agree with the rocFFT backend and the oracle."""
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=(25, 5, 3), partial=True)
+    out = []
+    for backend in ("engine", "rocfft"):
+        with Session(shape[::-1], fft_backend=backend, fft_pad_policy="fast") as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.OPTIMIZATION_I)
+            if backend == "engine":
+                assert s.fft_dims()[0] == lx
+            s.init_psi()
+            s.run(3, 0.006)
+            if backend == "engine":
+                assert s.xpass_mode() == 2, "x tile path not taken"
+            s.apply_mask()
+            out.append(s.get_psi())
+    assert rel_l2(out[0], out[1]) < 1e-5
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
+    assert rel_l2(out[0], res.psi) < TOL
+
+
 @pytest.mark.parametrize("shape,ksize", [((1, 16, 20), (5, 5, 3)), ((2, 12, 16), (3, 5, 3)),
                                          ((3, 10, 12), (3, 3, 5))])
 def test_thin_volumes(gpu, shape, ksize):
