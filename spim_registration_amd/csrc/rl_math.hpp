@@ -17,15 +17,34 @@ __device__ __forceinline__ int64_t mirror_idx(int64_t s, int64_t n) {
     return j >= n ? p - j : j;
 }
 
+// d / lambda rounded to nearest, as Java's double division, from inv = RN(1 / lambda):
+// q = d * inv lies within 1.5 ulp of d / lambda; the first fma correction makes it
+// faithful, the second (Markstein: r = d - lambda q is exact, inv within half an
+// ulp of 1 / lambda) correctly rounded.  5 double ops instead of the scaled division
+// sequence (2 div_scale, a quarter-rate rcp, 7 fma, div_fmas, div_fixup).  Operands
+// here: d = sqrt(1 + 2 lambda v) - 1 is 0 or in [2^-52, 2^512], lambda > 0 normal;
+// an infinite d keeps the quotient (the corrections would turn it into NaN).
+// (tests/test_oracle.py::test_tikhonov_division_correctly_rounded checks the sequence
+// against exact rational division)
+__device__ __forceinline__ double div_rn_by(double d, double lambda, double inv) {
+    const double q0 = d * inv;
+    const double r0 = __builtin_fma(-lambda, q0, d);
+    const double q1 = __builtin_fma(r0, inv, q0);
+    const double r1 = __builtin_fma(-lambda, q1, d);
+    const double q2 = __builtin_fma(r1, inv, q1);
+    return __builtin_isfinite(q0) ? q2 : q0;
+}
+
 // MVDeconvolution.computeNextValue (:671-703) with lambda's sign known at compile
 // time: the Tikhonov branch (double sqrt / divide) is not even if-converted into the
-// lambda = 0 kernels.
+// lambda = 0 kernels.  inv_lambda = 1.0 / lambda (hoisted by the caller).
 template <bool TIK>
-__device__ __forceinline__ float next_value_t(float last, float integral, float weight, double lambda) {
+__device__ __forceinline__ float next_value_t(float last, float integral, float weight, double lambda,
+                                              double inv_lambda) {
     const float value = __fmul_rn(last, integral);
     float adjusted;
     if (value > 0.0f) {
-        if constexpr (TIK) adjusted = (float)((sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0) / lambda);
+        if constexpr (TIK) adjusted = (float)div_rn_by(sqrt(1.0 + 2.0 * lambda * (double)value) - 1.0, lambda, inv_lambda);
         else adjusted = value;
     } else {
         adjusted = kMinValue;
@@ -36,8 +55,8 @@ __device__ __forceinline__ float next_value_t(float last, float integral, float 
 
 // Same, lambda tested at run time (lambda > 0: Tikhonov, MVDeconvolution.java:681-690)
 __device__ __forceinline__ float next_value(float last, float integral, float weight, double lambda) {
-    return lambda > 0.0 ? next_value_t<true>(last, integral, weight, lambda)
-                        : next_value_t<false>(last, integral, weight, lambda);
+    return lambda > 0.0 ? next_value_t<true>(last, integral, weight, lambda, 1.0 / lambda)
+                        : next_value_t<false>(last, integral, weight, lambda, 0.0);
 }
 
 }  // namespace spimdecon

@@ -61,6 +61,34 @@ def test_tikhonov_kat():
     assert abs(float(ref.tikhonov(1e-6, lam)) - 1e-6) < 1e-12
 
 
+@pytest.mark.parametrize("lam", [0.006, 0.0006, 0.05, 0.3, 1e-7])
+def test_tikhonov_division_correctly_rounded(lam):
+    """The engine divides d = sqrt(1 + 2 l v) - 1 by l as q0 = d * RN(1/l) plus two fma
+    corrections (rl_math.hpp div_rn_by).  Restated here with exact rational fma: it
+    must equal Java's correctly rounded double d / l (MVDeconvolution.java:681-690)
+    for float32 values over 2^-40 .. 2^20, and keep an infinite d infinite."""
+    from fractions import Fraction as Fr
+
+    def fma(a, b, c):
+        return float(Fr(a) * Fr(b) + Fr(c))
+
+    def div_rn_by(d, lam, inv):
+        q0 = d * inv
+        if not math.isfinite(q0):
+            return q0
+        q1 = fma(fma(-lam, q0, d), inv, q0)
+        return fma(fma(-lam, q1, d), inv, q1)
+
+    inv = 1.0 / lam
+    rng = np.random.default_rng(11)
+    vals = np.float32(2.0) ** rng.uniform(-40, 20, 6000).astype(np.float32)
+    vals = np.concatenate([vals, rng.random(2000, dtype=np.float32) * 4])
+    for v in vals:
+        d = math.sqrt(1.0 + 2.0 * lam * float(v)) - 1.0
+        assert div_rn_by(d, lam, inv) == d / lam, (float(v), lam)
+    assert div_rn_by(math.inf, lam, inv) == math.inf
+
+
 def test_compute_next_value_rules():
     """computeNextValue (:671-703): value <= 0 or NaN -> minValue; weight blend."""
     psi = np.float32([1.0, 1.0, 1.0, 2.0, 0.5])
