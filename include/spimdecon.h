@@ -129,6 +129,14 @@ int mvd_prepare_kernels(int nviews, const float* const* k1_in, const int* kdims,
                         int psftype, int ij_threads,
                         float* const* k1_out, float* const* k2_out, int devCUDA);
 
+/* out[i] = MVDeconvolution.computeNextValue(last[i], integral[i], weight[i])
+ * (MVDeconvolution.java:671-703; lambda > 0: the Tikhonov branch :681-690) for
+ * n voxels, DEVICE pointers on the current device -- the exact per-voxel rule the
+ * session's update step applies, exposed so callers and tests can check it bit for
+ * bit against the reference rule.  Synchronous. */
+int spimdecon_next_value(const float* last, const float* integral, const float* weight, int64_t n,
+                         double lambda, float* out);
+
 /* ======================================================================
  * 5. GPU-resident RL session (replaces MVDeconvolution.runIteration's
  *    per-view convolve1 -> quotient -> convolve2 -> update loop,

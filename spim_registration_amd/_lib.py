@@ -98,6 +98,7 @@ SIGNATURES = {
     "getFreeMemDeviceCUDA": (_i64, [C.c_int]),
     "getCUDAcomputeCapabilityMajorVersion": (C.c_int, [C.c_int]),
     "getCUDAcomputeCapabilityMinorVersion": (C.c_int, [C.c_int]),
+    "spimdecon_next_value": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_double, C.c_void_p]),
     "mvd_prepare_kernels": (C.c_int, [C.c_int, C.POINTER(_pf), _pi, C.c_int, C.c_int,
                                       C.POINTER(_pf), C.POINTER(_pf), C.c_int]),
     "mvd_params_default": (None, [C.POINTER(MvdParams)]),

@@ -133,6 +133,16 @@ int getCUDAcomputeCapabilityMinorVersion(int devCUDA) {
     return r;
 }
 
+int spimdecon_next_value(const float* last, const float* integral, const float* weight, int64_t n, double lambda,
+                         float* out) {
+    return guarded([&] {
+        SD_CHECK(n >= 0, SPIMDECON_ERR_ARG, "n must be >= 0");
+        SD_CHECK(n == 0 || (last && integral && weight && out), SPIMDECON_ERR_ARG, "null pointer");
+        launch_next_value(last, integral, weight, n, lambda, out, nullptr);
+        SD_HIP(hipStreamSynchronize(nullptr));
+    });
+}
+
 // ---------------------------------------------------------------- kernel preparation
 int mvd_prepare_kernels(int nviews, const float* const* k1_in, const int* kdims, int psftype,
                         int ij_threads, float* const* k1_out, float* const* k2_out, int devCUDA) {

@@ -441,6 +441,24 @@ void launch_swap_outer(const float* a, float* b, int64_t nx, int64_t ny, int64_t
     SD_HIP(hipGetLastError());
 }
 
+// out[i] = computeNextValue(last[i], integral[i], weight[i]) -- the per-voxel rule of
+// both update paths, exposed for bit-exact checks against the reference rule
+__global__ __launch_bounds__(kBlock) void k_next_value(const float* __restrict__ last,
+                                                       const float* __restrict__ integ,
+                                                       const float* __restrict__ w, int64_t n, double lambda,
+                                                       float* __restrict__ out) {
+    const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (i < n) out[i] = next_value(last[i], integ[i], w[i], lambda);
+}
+
+void launch_next_value(const float* last, const float* integral, const float* weight, int64_t n, double lambda,
+                       float* out, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_next_value, dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, last, integral,
+                       weight, n, lambda, out);
+    SD_HIP(hipGetLastError());
+}
+
 void launch_to_half(const float* in, void* out, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_to_half, dim3(grid_for(n, 256)), dim3(256), 0, s, in,
                        static_cast<__half*>(out), n);

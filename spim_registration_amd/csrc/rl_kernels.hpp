@@ -35,6 +35,10 @@ int64_t launch_update_pad(const SlabGeom& g, Store st, const float* psi_in, cons
                           const void* w, double lambda, float* psi_out, float* Ra,
                           double* partials, bool write_pad, hipStream_t s);
 
+// out[i] = the RL update rule (MVDeconvolution.computeNextValue) of voxel i, device arrays
+void launch_next_value(const float* last, const float* integral, const float* weight, int64_t n, double lambda,
+                       float* out, hipStream_t s);
+
 // out[0] += sum(partials[2i]), out[1] = max(out[1], max(partials[2i+1])) -- single block,
 // deterministic order.  `accumulate` = 0 overwrites out.
 void launch_reduce_partials(const double* partials, int64_t nblocks, double* out, int accumulate,

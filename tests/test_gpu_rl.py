@@ -366,3 +366,31 @@ def test_thin_volumes(gpu, shape, ksize):
     res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
     assert np.isfinite(psi).all()
     assert rel_l2(psi, res.psi) < TOL
+
+
+@pytest.mark.parametrize("lam", [0.0, 0.006, 0.0006, 0.3, 1e-7])
+def test_next_value_rule_bit_exact(gpu, lam):
+    """spimdecon_next_value (the per-voxel update rule of both update paths:
+    Tikhonov sqrt and division by lambda included) against the oracle's
+    computeNextValue (MVDeconvolution.java:671-703), bit for bit, over random
+    voxels and the special cases: value <= 0, NaN, +-inf, denormal, huge."""
+    import torch
+    from spim_registration_amd import _lib
+    rng = np.random.default_rng(3)
+    n = 1 << 20
+    last = (rng.random(n, dtype=np.float32) * 10).astype(np.float32)
+    integ = (np.float32(2.0) ** rng.uniform(-40, 40, n)).astype(np.float32)
+    integ[: n // 8] = rng.standard_normal(n // 8).astype(np.float32)
+    special = np.float32([0.0, -0.0, -1.0, np.nan, np.inf, -np.inf, 1e-45, 1e-38, 3e38, 1.0])
+    integ[n // 8: n // 8 + special.size] = special
+    w = rng.random(n, dtype=np.float32)
+    w[:16] = [0.0, 1.0] * 8
+    d = [torch.from_numpy(a).cuda() for a in (last, integ, w)]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    _lib.check(_lib.load().spimdecon_next_value(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n, lam,
+                                                  out.data_ptr()))
+    got = out.cpu().numpy()
+    want = ref.compute_next_value(last, integ, w, lam)
+    nan = np.isnan(want)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint32), want[~nan].view(np.uint32))
