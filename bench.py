@@ -91,13 +91,13 @@ def pmc_traffic(cls, M, args):
             targs = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
             if cls == "z_convolve" and name.startswith("k_col2f") and targs[3] not in ("2", "4", "5"):
                 continue   # the fused z pass: k_col2f MODE 2/4/5 (5 = compact kernels)
-            hits.append((name, int(ent["hbm_bytes_per_launch"])))
+            hits.append((name, int(ent.get("hbm_bytes_per_launch_median", ent["hbm_bytes_per_launch"]))))
     if not hits:
         return None, None
     if cls == "z_convolve":
         hits = hits[:1]
     return (int(sum(b for _, b in hits) / len(hits)),
-            "profiles/pmc_traffic.json: " + " / ".join(n for n, _ in hits) + (" (mean)" if len(hits) > 1 else ""))
+            "profiles/pmc_traffic.json: " + " / ".join(n for n, _ in hits) + (" (mean of the median launches)" if len(hits) > 1 else " (median launch)"))
 
 
 def cpu_model():

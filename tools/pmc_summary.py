@@ -52,7 +52,12 @@ def main(out, json_out=None, dims=None, fp16=False):
         row = [k, f"{t * 1e6:.1f}", f"{traffic / 1e6:.1f}", f"{traffic / t / 1e9:.0f}"]
         row += [f"{avg(v.get(c, [])):.3g}" for c in cols]
         print("| " + " | ".join(row) + " |")
+        med = lambda xs: sorted(xs)[len(xs) // 2] if xs else float("nan")
+        # median launch: a kernel name can also cover short launches (the y pass of the
+        # compact kernel spectra, 2kc+1 planes) that pull the mean below a data pass
+        tmed = (2 * med(v.get("FETCH_SIZE", [])) + med(v.get("WRITE_SIZE", []))) * 1024
         table[k] = {"avg_us": round(t * 1e6, 2), "hbm_bytes_per_launch": int(traffic),
+                    "hbm_bytes_per_launch_median": int(tmed),
                     "fetch_kb_x2": 2 * fetch, "write_kb": write}
     if json_out:
         import json
