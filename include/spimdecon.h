@@ -196,6 +196,18 @@ void mvd_destroy(mvd_session* h);
 /* devices of the session and the device holding slab s (slabs: ndev * local_slabs) */
 int  mvd_num_devices(mvd_session* h, int* ndev);
 int  mvd_slab_device(mvd_session* h, int slab, int* dev);
+/* slabs of the session: ndev * local_slabs, where local_slabs may exceed
+ * params.local_slabs -- the engine splits a device's share further until every
+ * slab buffer (psi, views, spectra) stays below 4 GiB, the range of its 32-bit
+ * buffer offsets (env SPIMDECON_AUTO_SLABS=0 disables; the slabs are exact, like
+ * the reference's precise blocks, BlockGeneratorFixedSizePrecise.java:25-101) */
+int  mvd_num_slabs(mvd_session* h, int* nslabs);
+/* voxels {nx, ny, nz} of slab s in the session's internal order (a y-split session
+ * keeps (x, z, y-slab) rows: nz is then the slab's y extent) */
+int  mvd_slab_extent(mvd_session* h, int slab, int64_t* out3);
+/* halo exchange counters since mvd_create: bytes and copies moved between slabs
+ * (local copies, peer pulls between device groups, RCCL sends); either may be NULL */
+int  mvd_exchange_stats(mvd_session* h, int64_t* bytes, int64_t* copies);
 
 /* Adds one view (MVDeconInput.add order).  img/weight: this rank's z-range,
  * dims = params.dims; kernel1: raw (un-normalised) PSF of kdims {kx,ky,kz}.

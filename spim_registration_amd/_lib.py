@@ -109,6 +109,9 @@ SIGNATURES = {
     "mvd_destroy": (None, [C.c_void_p]),
     "mvd_num_devices": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "mvd_slab_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "mvd_num_slabs": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    "mvd_slab_extent": (C.c_int, [C.c_void_p, C.c_int, _pi64]),
+    "mvd_exchange_stats": (C.c_int, [C.c_void_p, _pi64, _pi64]),
     "mvd_add_view": (C.c_int, [C.c_void_p, _pf, _pf, _pf, _pi]),
     "mvd_add_view_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, _pf, _pi]),
     "mvd_init": (C.c_int, [C.c_void_p, C.c_int]),

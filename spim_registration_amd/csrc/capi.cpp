@@ -311,6 +311,18 @@ int mvd_slab_device(mvd_session* h, int slab, int* dev) {
     return guarded([&] { SESSION(h); SD_CHECK(dev, SPIMDECON_ERR_ARG, "null"); *dev = S.slab_device(slab); });
 }
 
+int mvd_num_slabs(mvd_session* h, int* nslabs) {
+    return guarded([&] { SESSION(h); SD_CHECK(nslabs, SPIMDECON_ERR_ARG, "null"); *nslabs = S.nslabs(); });
+}
+
+int mvd_exchange_stats(mvd_session* h, int64_t* bytes, int64_t* copies) {
+    return guarded([&] { SESSION(h); S.exchange_stats(bytes, copies); });
+}
+
+int mvd_slab_extent(mvd_session* h, int slab, int64_t* out3) {
+    return guarded([&] { SESSION(h); SD_CHECK(out3, SPIMDECON_ERR_ARG, "null"); S.slab_extent(slab, out3); });
+}
+
 int mvd_enable_timing(mvd_session* h, int on) {
     return guarded([&] { SESSION(h); S.enable_timing(on != 0); });
 }

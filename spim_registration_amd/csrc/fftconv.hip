@@ -774,6 +774,15 @@ int64_t engine_fast_size(int64_t need, bool even, int policy) {
     return fast * 4 <= smooth * 5 ? fast : smooth;
 }
 
+bool engine_slab_fits(int64_t nx, int64_t ny, int64_t nzs, const int halo[3], int policy) {
+    const int64_t Mx = engine_fast_size(nx + 2 * halo[0], true, policy);
+    const int64_t My = engine_fast_size(ny + 2 * halo[1], false, policy);
+    const int64_t Mz = engine_fast_size(nzs + 2 * halo[2], false, policy);   // >= the exact nz + 2 cz
+    const int64_t Hp = ceil_div(Mx / 2 + 1, int64_t(16)) * 16;
+    return uint64_t(nx) * uint64_t(ny) * uint64_t(nzs) * 4u < kOOB &&
+           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) < kOOB;
+}
+
 void SpectralPlan::create(const SlabGeom& geom, bool allow_2f, bool z_fft) {
     g = geom;
     SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");

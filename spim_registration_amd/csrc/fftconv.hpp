@@ -63,6 +63,11 @@ struct SpectralPlan {
 // 2: always the smooth size.
 int64_t engine_fast_size(int64_t need, bool even, int policy = 0);
 
+// true when a slab of nx * ny * nzs voxels with kernel half sizes <= halo keeps every
+// buffer the fast passes address (psi, views, spectra) inside their 32-bit offset
+// range; the session splits a device's share into more slabs until it does
+bool engine_slab_fits(int64_t nx, int64_t ny, int64_t nzs, const int halo[3], int policy);
+
 // ---- passes (all asynchronous on `s`) ----
 // psi -> C (x-spectra of the mirror-extended psi rows)
 void engine_forward_psi(const SpectralPlan& p, const float* psi, float2* C, hipStream_t s);

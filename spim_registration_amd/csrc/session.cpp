@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -73,6 +75,30 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
     SD_CHECK(G == 1 || p.nranks == 1, SPIMDECON_ERR_ARG,
              "several devices per process and several RCCL ranks cannot be combined");
     SD_CHECK(G == 1 || p.fft_backend == 0, SPIMDECON_ERR_ARG, "several devices need the engine backend");
+    // Engine slabs whose buffers outgrow the 32-bit offsets of the fast passes (a 1024^3
+    // psi is 2^32 B) are split further on their device: exact slabs with halos, the
+    // same arithmetic as any other split.  Kernel half sizes are not known yet: up to
+    // 16 (33-plane kernels) is assumed unless mvd_params.halo says more.  An automatic
+    // split axis is re-decided for the new slab count (the longer of y and z).
+    static const bool auto_slabs = [] {
+        const char* e = std::getenv("SPIMDECON_AUTO_SLABS");
+        return !(e && e[0] == '0');
+    }();
+    if (p0.fft_backend == 0 && auto_slabs && p0.local_slabs >= 1) {
+        auto needed = [&](const mvd_params& q, int ls) {
+            const int hal[3] = {std::max(q.halo[0], 16), std::max(q.halo[1], 16), std::max(q.halo[2], 16)};
+            while (ls < q.dims[2] && !engine_slab_fits(q.dims[0], q.dims[1], ceil_div(q.dims[2], int64_t(G) * ls),
+                                                       hal, q.fft_pad_policy))
+                ++ls;
+            return ls;
+        };
+        int ls = needed(p_, p0.local_slabs);
+        if (ls != p0.local_slabs && p0.slab_axis == -1) {
+            p_ = internal_params(p0, G * ls, &axis_);
+            ls = needed(p_, ls);
+        }
+        p_.local_slabs = ls;
+    }
     const int nslabs = G * p.local_slabs;
     SD_CHECK(nslabs <= p.dims[2], SPIMDECON_ERR_ARG, "more slabs than z planes");
     if (p_.nz_global <= 0) p_.nz_global = p.dims[2];
@@ -164,6 +190,19 @@ Session::~Session() {
 int Session::slab_device(int slab) const {
     SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
     return groups_[slabs_[slab].grp].dev;
+}
+
+void Session::exchange_stats(int64_t* bytes, int64_t* copies) const {
+    if (bytes) *bytes = xbytes_.load();
+    if (copies) *copies = xcopies_.load();
+}
+
+void Session::slab_extent(int slab, int64_t* out3) const {
+    SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
+    const SlabGeom& g = slabs_[slab].g;
+    out3[0] = g.nx;
+    out3[1] = g.ny;
+    out3[2] = g.nz;
 }
 
 void Session::sync_all() {
@@ -461,6 +500,7 @@ double Session::init_psi(const float* psi_or_null) {
     }
     sync_all();
     psi_ready_ = true;
+    poisoned_ = false;  // every slab holds the same (new) starting psi again
     return avg;
 }
 
@@ -544,6 +584,8 @@ void Session::exchange(bool which, hipStream_t st) {
                               get(lo) + size_t(lo.g.nz - cz) * plane, bytes,
                               hipMemcpyDeviceToDevice, st));
     }
+    xbytes_ += int64_t(2) * (S - 1) * int64_t(bytes);
+    xcopies_ += int64_t(2) * (S - 1);
     if (p_.nranks > 1) {
         const size_t count = size_t(cz) * plane;
         SD_NCCL(ncclGroupStart());
@@ -561,6 +603,9 @@ void Session::exchange(bool which, hipStream_t st) {
                              comm_, st));
         }
         SD_NCCL(ncclGroupEnd());
+        const int nsend = (p_.rank > 0 ? 1 : 0) + (p_.rank < p_.nranks - 1 ? 1 : 0);
+        xbytes_ += int64_t(nsend) * int64_t(count * sizeof(float));
+        xcopies_ += nsend;
     }
     tstop(st);
 }
@@ -598,6 +643,9 @@ void Session::group_exchange_begin(int gi, bool which, HostBarrier& bar) {
                 SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + size_t(me.g.nz) * plane,
                                       buf_ptr(hi, which, backend_), bytes, hipMemcpyDefault, gr.xstream));
             }
+            const int npull = (s > 0 ? 1 : 0) + (s < S - 1 ? 1 : 0);
+            xbytes_ += int64_t(npull) * int64_t(bytes);
+            xcopies_ += npull;
         }
     }
     if (gi == 0) tstop(gr.xstream);
@@ -633,6 +681,7 @@ void Session::allreduce_max(double* host, int n) {
 }
 
 void Session::run(int iters, double lambda, double* stats) {
+    SD_CHECK(!poisoned_, SPIMDECON_ERR_STATE, "an earlier multi-device run failed mid-iteration; destroy the session");
     SD_CHECK(iters >= 0, SPIMDECON_ERR_ARG, "iters must be >= 0");
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "call mvd_init (or mvd_set_kernels) first");
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "call mvd_init_psi first");
@@ -642,14 +691,37 @@ void Session::run(int iters, double lambda, double* stats) {
         DeviceGuard guard(gr.dev);
         gr.stats.alloc(size_t(iters) * V * 2);
     }
-    if (backend_ == 1) {
-        DeviceGuard guard(p_.device);
-        run_rocfft(iters, lambda);
-    } else if (groups_.size() == 1) {
-        DeviceGuard guard(p_.device);
-        run_engine(0, iters, lambda, nullptr);
-    } else {
-        run_groups(iters, lambda);
+    try {
+        if (backend_ == 1) {
+            DeviceGuard guard(p_.device);
+            run_rocfft(iters, lambda);
+        } else if (groups_.size() == 1) {
+            DeviceGuard guard(p_.device);
+            run_engine(0, iters, lambda, nullptr);
+        } else {
+            run_groups(iters, lambda);
+        }
+    } catch (...) {
+        if (slabs_.size() > 1 || p_.nranks > 1) poisoned_ = true;
+        throw;
+    }
+    if (backend_ == 0 && !warned_fallback_) {
+        // the fast paths are a layout choice, not a semantic one: a slab outside them runs
+        // the Stockham passes with the same results, several times slower -- say so once
+        for (int s = 0; s < int(slabs_.size()); ++s) {
+            const int xm = slabs_[s].sp.xmode_update, zm = zpass_mode(s);
+            if (xm != 2 || (zm != 2 && zm != 3)) {
+                std::fprintf(stderr,
+                             "[spimdecon] warning: slab %d (%lld x %lld x %lld, padded %lld x %lld x %lld) runs "
+                             "outside the fast engine passes (x pass %d, z pass %d; fast = 2 and 2/3): same "
+                             "results, lower throughput\n",
+                             s, (long long)slabs_[s].g.nx, (long long)slabs_[s].g.ny, (long long)slabs_[s].g.nz,
+                             (long long)slabs_[s].g.Mx, (long long)slabs_[s].g.My, (long long)slabs_[s].g.Mz, xm,
+                             zm);
+                warned_fallback_ = true;
+                break;
+            }
+        }
     }
     // per-group {sum, max} -> totals (sum over groups in double, max)
     std::vector<double> st(size_t(iters) * V * 2, 0.0), part(st.size());
@@ -711,6 +783,8 @@ void Session::run_groups(int iters, double lambda) {
         });
     }
     for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (e) poisoned_ = true;  // the groups stopped at different views / iterations
     for (auto& e : errs)  // the first failure that is not another group's abort
         if (e) {
             try {
@@ -922,6 +996,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
 }
 
 void Session::apply_mask() {
+    SD_CHECK(!poisoned_, SPIMDECON_ERR_STATE, "an earlier multi-device run failed mid-iteration; psi is inconsistent");
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
     for (auto& sl : slabs_) {
         DeviceGuard guard(groups_[sl.grp].dev);
@@ -931,6 +1006,7 @@ void Session::apply_mask() {
 }
 
 void Session::get_psi(float* out) {
+    SD_CHECK(!poisoned_, SPIMDECON_ERR_STATE, "an earlier multi-device run failed mid-iteration; psi is inconsistent");
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "psi not initialised");
     SD_CHECK(out, SPIMDECON_ERR_ARG, "null output");
     for (auto& sl : slabs_) {

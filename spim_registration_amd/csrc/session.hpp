@@ -23,6 +23,7 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -112,6 +113,10 @@ public:
     int xpass_mode(int slab) const;
     hipStream_t stream() const { return groups_[0].stream; }
     int ndevices() const { return int(groups_.size()); }
+    int nslabs() const { return int(slabs_.size()); }
+    void slab_extent(int slab, int64_t* out3) const;
+    // halo bytes / copies moved between slabs (local, peer or RCCL sends) since creation
+    void exchange_stats(int64_t* bytes, int64_t* copies) const;
     int slab_device(int slab) const;
     void enable_timing(bool on) { timing_on_ = on; }
     void timing(double* out16);
@@ -160,6 +165,11 @@ private:
     bool kernels_ready_ = false;
     bool spectra_ready_ = false;
     bool psi_ready_ = false;
+    // a multi-device run aborted mid-iteration: the slabs hold psi of different
+    // iterations, so nothing but destruction is allowed afterwards
+    bool poisoned_ = false;
+    bool warned_fallback_ = false;  // the Stockham-fallback warning is printed once
+    std::atomic<int64_t> xbytes_{0}, xcopies_{0};  // (group threads add concurrently)
     bool timing_on_ = false;
     std::vector<TimingRec> trecs_;
     int tcur_ = -1;

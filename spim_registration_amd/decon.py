@@ -278,6 +278,26 @@ class Session:
         check(self.lib.mvd_slab_device(self.h, int(slab), C.byref(out)))
         return out.value
 
+    def num_slabs(self):
+        """slabs of the session (devices x local slabs, after the automatic split of
+        slabs whose buffers exceed the fast passes' 32-bit offsets)."""
+        out = C.c_int()
+        check(self.lib.mvd_num_slabs(self.h, C.byref(out)))
+        return out.value
+
+    def exchange_stats(self):
+        """(bytes, copies) of halo planes moved between slabs since creation."""
+        b, c = C.c_int64(), C.c_int64()
+        check(self.lib.mvd_exchange_stats(self.h, C.byref(b), C.byref(c)))
+        return b.value, c.value
+
+    def slab_extent(self, slab=0):
+        """voxels (nx, ny, nz) of a slab in the session's internal order (y-split
+        sessions: (x, z, y-slab))."""
+        out = (C.c_int64 * 3)()
+        check(self.lib.mvd_slab_extent(self.h, int(slab), out))
+        return tuple(out)
+
     def enable_timing(self, on=True):
         check(self.lib.mvd_enable_timing(self.h, int(on)))
 

@@ -55,7 +55,8 @@ def run_to_host(imgs, ws, psfs, psftype, iters, lam, **kw):
     with session_from_device(imgs, ws, psfs, psftype, **kw) as s:
         st = s.run(iters, lam)
         s.apply_mask()
-        info = {"fft_dims": s.fft_dims(0), "zpass": s.zpass_mode(0), "xpass": s.xpass_mode(0)}
+        info = {"fft_dims": s.fft_dims(0), "zpass": s.zpass_mode(0), "xpass": s.xpass_mode(0),
+                "slabs": s.num_slabs(), "extent0": s.slab_extent(0)}
         return s.get_psi(), st, info
 
 
@@ -130,10 +131,11 @@ def test_c3_6view_1024x1024x512_tikhonov_20_iterations(gpu):
                                                 device="cuda:0")
     release()
     args = (imgs, ws, psfs, PSFTYPE.EFFICIENT_BAYESIAN, 20, 0.006)
-    # the 8-GPU decomposition (8 z-slabs of 64 planes, halo pulls between device
-    # groups), all groups on this GPU
-    psi8, st8, _ = run_to_host(*args, devices=[0] * 8)
+    # the 8-GPU decomposition (the longer axis: 8 y-slabs of 128 rows, kept as (x, z, y)
+    # rows; halo pulls between device groups), all groups on this GPU
+    psi8, st8, info8 = run_to_host(*args, devices=[0] * 8)
     release()
+    assert info8["slabs"] == 8 and info8["extent0"] == (1024, 512, 128), info8
     # one slab of 1024x1024x512: spectra of 2.38 GB on the fast engine passes
     psi1, st1, info1 = run_to_host(*args)
     release()

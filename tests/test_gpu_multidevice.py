@@ -172,3 +172,39 @@ def test_y_split_fp16_initial_image_and_kernels(gpu):
     assert rel_l2(out[1][0], out[0][0]) < 1e-5
     np.testing.assert_array_equal(out[1][1], out[0][1])
     np.testing.assert_array_equal(out[1][2], out[0][2])
+
+
+@pytest.mark.timeout(600)
+def test_c3_strong_decomposition_exchange_accounting(gpu):
+    """BASELINE configs[2] as the 8-GPU strong decomposition (8 device groups, all on
+    this GPU): 8 y-slabs of 128 rows, one halo exchange of every boundary in both
+    directions per pad (the initial psi pad, then the quotient and the next psi per
+    view; the last update pads nothing): 2 * iters * V exchanges of 2 * 7 copies of
+    cz planes each.  Prints the exchange time the timing class measured."""
+    import torch
+    imgs, ws, psfs = synthetic.make_views_torch((512, 1024, 1024), 6, config_id=3, ksize=(25, 25, 25),
+                                                device="cuda:0")
+    iters, V, G = 2, 6, 8
+    with Session((1024, 1024, 512), devices=[0] * G) as s:
+        for i, w, k in zip(imgs, ws, psfs):
+            s.add_view_device(i.data_ptr(), w.data_ptr(), k)
+        del imgs, ws
+        torch.cuda.empty_cache()
+        s.init(PSFTYPE.EFFICIENT_BAYESIAN)
+        s.init_psi()
+        assert s.num_slabs() == G and s.slab_extent(0) == (1024, 512, 128)
+        Mx, My, Mz = s.fft_dims(0)
+        Hp = -(-(Mx // 2 + 1) // 16) * 16
+        plane = 2 * Hp * My * 4                      # bytes of one padded x-spectrum plane
+        cz = 12                                      # 25-plane kernels
+        b0, c0 = s.exchange_stats()
+        s.enable_timing(True)
+        s.run(iters, 0.006)
+        tm = s.timing()
+        b1, c1 = s.exchange_stats()
+        copies = 2 * iters * V * 2 * (G - 1)
+        assert c1 - c0 == copies, (c1 - c0, copies)
+        assert b1 - b0 == copies * cz * plane, (b1 - b0, copies * cz * plane)
+        assert tm[8 + 5] == 2 * iters * V               # group 0's exchange intervals
+        print(f"\nC3 8-group exchange: {plane * cz / 1e6:.1f} MB per copy, {(b1 - b0) / iters / 1e9:.2f} GB "
+              f"per iteration (all boundaries), {tm[5] / tm[13]:.3f} ms per exchange on group 0's stream")
