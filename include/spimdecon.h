@@ -38,6 +38,7 @@ extern "C" {
 #define SPIMDECON_ERR_COMM        -5
 #define SPIMDECON_ERR_STATE       -6
 #define SPIMDECON_ERR_OOM         -7
+#define SPIMDECON_ERR_IO          -8   /* file cannot be opened (Java: IOException) */
 
 /* last error message of the calling thread ("" if none) */
 const char* spimdecon_last_error(void);

@@ -199,6 +199,9 @@ def last_error() -> str:
     return load().spimdecon_last_error().decode(errors="replace")
 
 
+ERR_IO = -8   # SPIMDECON_ERR_IO: a file that cannot be opened
+
+
 def check(status: int):
     if status != 0:
         raise SpimDeconError(status, last_error())

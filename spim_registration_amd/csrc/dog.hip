@@ -356,8 +356,10 @@ constexpr int kDxyTX = 64;   // xy tile: outputs along x (TY along y: template)
 constexpr int kDxySeg = 8;   // x outputs per thread in the x phase (register window)
 constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave per row, the
                              // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
-constexpr int kDzPD = 3;     // planes loaded ahead of use
+constexpr int kDzPD = 8;     // planes loaded ahead of use: 3 left the HBM latency exposed
+                             // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 64; // DoG planes per block (the window adds KW - 1 + 2 loads)
+constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
 
 __device__ __forceinline__ int mirror32(int i, int n) {
     bool o;
@@ -368,60 +370,121 @@ __device__ __forceinline__ int mirror32(int i, int n) {
 // would also wait for the planes loaded ahead)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// LDS pitch (floats) of the staged input rows of k_dog_xy: >= iw, a multiple of 4 (16-B
+// aligned rows for the b128 window reads) and 4 * odd modulo 64, so that the 16 lanes of a
+// ds_read_b128 group -- 16 consecutive rows of one segment, rows mod 16 all distinct --
+// start on 16 distinct 4-bank groups (MI355X_MICROARCH.md LDS table): conflict-free
+__host__ __device__ constexpr int dxy_in_pitch(int iw) {
+    int p = (iw + 3) / 4 * 4;
+    while ((p / 4) % 2 == 0) p += 4;
+    return p;
+}
+// row pitch (float2) of the x-phase results: 64 + 2, so the 8 consecutive rows of a
+// ds_write_b128 group land on 8 distinct 4-bank groups mod 32
+constexpr int kDxySxP = kDxyTX + 2;
+
+// (v - mn) / diff correctly rounded (__fdiv_rn's result) from the reciprocal rd = RN(1/diff):
+// q = v * rd, then two Markstein corrections q += (a - q * diff) * rd with exact fma
+// residuals -- the second starts from a faithful quotient, so it rounds correctly
+// (Markstein's theorem; the Tikhonov step, rl_math.hpp, uses the same scheme in double).
+// Outside the range where the residuals are exact (0, tiny, huge or non-finite a) the
+// IEEE division itself.  5 VALU instead of the ~10 of the scaled division sequence.
+__device__ __forceinline__ float div_rn_rcp(float a, float diff, float rd) {
+    const float aa = fabsf(a);
+    if (!(aa >= 0x1p-48f && aa <= 0x1p48f)) return __fdiv_rn(a, diff);   // q and residuals stay normal
+    float q = __fmul_rn(a, rd);
+    q = __fmaf_rn(__fmaf_rn(-q, diff, a), rd, q);
+    return __fmaf_rn(__fmaf_rn(-q, diff, a), rd, q);
+}
+
+// The box of a k_dog_z block.  With `xcd` the dispatch order is remapped so that each
+// XCD (blocks go round-robin to the 8 XCDs, each with its own L2) walks a contiguous
+// range of boxes with y fastest: the boxes it holds at once are y-neighbours, whose
+// overlapping halo rows (2 of every BY) then come from that L2 instead of HBM.
+// (k_dog_xy: x fastest, so each XCD's resident tiles share their x and y halo columns.)
+struct DzBox { int bx, by, bz; };
+template <bool YFAST>
+__device__ __forceinline__ DzBox xcd_box(bool xcd) {
+    if (!xcd) return {int(blockIdx.x), int(blockIdx.y), int(blockIdx.z)};
+    const unsigned gx = gridDim.x, gy = gridDim.y;
+    const unsigned n = gx * gy * gridDim.z;
+    const unsigned lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const unsigned k = lin & 7u, j = lin >> 3, q = n >> 3, r = n & 7u;
+    const unsigned l = k * q + min(k, r) + j;           // XCD k: logical boxes [k q + min(k, r), ...)
+    if (YFAST) return {int((l / gy) % gx), int(l % gy), int(l / (gy * gx))};
+    return {int(l % gx), int((l / gx) % gy), int(l / (gx * gy))};
+}
+
 template <int KW, int TY>
 __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
-                                                const float* __restrict__ mm) {
+                                                const float* __restrict__ mm, int xcd) {
     constexpr int R = KW / 2;
     constexpr int IW = kDxyTX + KW - 1;          // staged input columns
-    constexpr int IP = (IW + 3) / 4 * 4;         // pitch: 16-B aligned rows
+    constexpr int IP = dxy_in_pitch(IW);         // pitch (see dxy_in_pitch)
     constexpr int IH = TY + KW - 1;              // staged input rows
+    constexpr int IHP = (IH + 63) / 64 * 64;     // x phase: rows padded to whole waves
     constexpr int NSEG = kDxyTX / kDxySeg;
     constexpr int WX = kDxySeg + KW - 1;
     constexpr int OY = TY / 4;                   // y outputs per thread (4 runs per column)
     constexpr int WY = OY + KW - 1;
     __shared__ __attribute__((aligned(16))) float sin_[IH * IP];
-    __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxyTX];
+    __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxySxP];
     const int nx = int(d.nx), ny = int(d.ny);
-    const int x0 = int(blockIdx.x) * kDxyTX, y0 = int(blockIdx.y) * TY;
-    const uint32_t plane = uint32_t(blockIdx.z) * uint32_t(ny) * uint32_t(nx);
+    const DzBox bb = xcd_box<false>(xcd != 0);
+    const int x0 = bb.bx * kDxyTX, y0 = bb.by * TY;
+    const uint32_t plane = uint32_t(bb.bz) * uint32_t(ny) * uint32_t(nx);
     const int t = threadIdx.x;
     // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
     bool norm = false;
-    float mn = 0.0f, diff = 1.0f;
+    float mn = 0.0f, diff = 1.0f, rd = 1.0f;
     if (mm) {
         mn = mm[0];
         diff = __fsub_rn(mm[1], mn);
         norm = !(isnan(diff) || isinf(diff) || diff == 0.0f);
+        rd = __frcp_rn(diff);
+        if (!(fabsf(diff) >= 0x1p-48f && fabsf(diff) <= 0x1p48f)) rd = 0.0f;   // (division only)
     }
     // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
     // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
     // load; every load in flight before the first use (a load per round trip exposed
-    // the HBM latency ~19 times per tile)
+    // the HBM latency ~19 times per tile).  Tiles whose staged box lies inside the
+    // volume (all but the outer ring of tiles) index without the mirror arithmetic.
     constexpr int RPT = 256 / IW;                // rows staged per pass
     constexpr int IPC = 256 / RPT;               // threads per row (>= IW)
     constexpr int NE = (IH + RPT - 1) / RPT;     // rows per thread
     const int col = t % IPC, r0 = t / IPC;
     const bool cact = col < IW && r0 < RPT;
-    const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
+    const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && y0 - R >= 0 && y0 - R + IH <= ny;
     float v[NE];
+    if (inside) {
+        const uint32_t base = plane + uint32_t(y0 - R) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
 #pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int row = min(r0 + RPT * e, IH - 1);
-        v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
+        for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
+    } else {
+        const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int row = min(r0 + RPT * e, IH - 1);
+            v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
+        }
     }
     if (cact) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int row = r0 + RPT * e;
             if (row >= IH) break;
-            sin_[row * IP + col] = norm ? __fdiv_rn(__fsub_rn(v[e], mn), diff) : v[e];
+            sin_[row * IP + col] = norm ? (rd != 0.0f ? div_rn_rcp(__fsub_rn(v[e], mn), diff, rd)
+                                                      : __fdiv_rn(__fsub_rn(v[e], mn), diff))
+                                        : v[e];
         }
     }
     __syncthreads();
-    // x phase: every staged row, kDxySeg outputs per thread from a window of WX values
-    for (int it = t; it < IH * NSEG; it += 256) {
-        const int row = it / NSEG, seg = it - row * NSEG;
+    // x phase: lane = staged row, the wave's segment of kDxySeg outputs from a window of
+    // WX values (b128 reads conflict-free through the pitch IP)
+    for (int it = t; it < IHP * NSEG; it += 256) {
+        const int row = it % IHP, seg = it / IHP;
+        if (row >= IH) continue;
         const float* src = sin_ + row * IP + seg * kDxySeg;
         float w[WX];
 #pragma unroll
@@ -435,7 +498,7 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
 #pragma unroll
             for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
         }
-        float2* dst = sx + row * kDxyTX + seg * kDxySeg;
+        float2* dst = sx + row * kDxySxP + seg * kDxySeg;
 #pragma unroll
         for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
     }
@@ -447,7 +510,7 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     dg_v2 w[WY];
 #pragma unroll
     for (int i = 0; i < WY; ++i) {
-        const float2 v = sx[(run * OY + i) * kDxyTX + c];
+        const float2 v = sx[(run * OY + i) * kDxySxP + c];
         w[i] = dg_v2{v.x, v.y};
     }
     dg_v2 acc[OY];
@@ -551,40 +614,65 @@ __device__ __forceinline__ void cand_flush(const PeakSink& pk, const int4* buf, 
 // 26-neighbour test is min / max of the 3x3x3 box (the box includes the centre, so
 // "all neighbours >= c" <=> box min >= c); a plane holding a NaN takes the
 // reference's comparison loop instead (NaN compares false).
-template <int KW, int BY>
+// InteractiveIntegral.isSpecialPoint (:443-468) over the 4-plane ring Dr[4][by][kDzBX]
+// (centre plane zc, row ty, column tx): 2 = every neighbour >= c ("MAX"), 1 = every
+// neighbour <= c, 0 = neither.  Only for boxes holding a NaN (compares false), out of
+// line: the min / max test covers every other box.
+__device__ __noinline__ int dz_special_nan(const float* Dr, int by, int zc, int ty, int tx, float c) {
+    bool ge = true, le = true;
+    for (int dz = -1; dz <= 1; ++dz)
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                if (dz == 0 && dy == 0 && dx == 0) continue;
+                const float v = Dr[(((zc + dz) & 3) * by + ty + dy) * kDzBX + tx + dx];
+                ge &= v >= c;
+                le &= v <= c;
+            }
+    return ge ? 2 : (le ? 1 : 0);
+}
+
+template <int KW, int BY, int PD>
 __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
                                                          const float2* __restrict__ kz, float scale, int zc_len,
-                                                         float* __restrict__ dog, PeakSink pk) {
+                                                         float* __restrict__ dog, PeakSink pk, int xcd) {
     constexpr int R = KW / 2;
-    constexpr int NW = KW + kDzPD;
+    constexpr int NW = KW + PD;
     __shared__ float Dr[4][BY][kDzBX];
     __shared__ int nanq[4];
     __shared__ int4 cbuf[BY][kCandBuf];   // one candidate buffer per wave (= row ty)
     int ccount = 0;                       // wave-uniform fill of this wave's buffer
     const int t = threadIdx.x, tx = t & (kDzBX - 1), ty = t / kDzBX;
     const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
-    const int X0 = int(blockIdx.x) * (kDzBX - 2), Y0 = int(blockIdx.y) * (BY - 2);
+    const DzBox bb = xcd_box<true>(xcd != 0);
+    const int X0 = bb.bx * (kDzBX - 2), Y0 = bb.by * (BY - 2);
     const int x = X0 + tx, y = Y0 + ty;
     const bool valid = x < nx && y < ny;
-    const int z0 = int(blockIdx.z) * zc_len, z1 = min(nz, z0 + zc_len);
+    const int z0 = bb.bz * zc_len, z1 = min(nz, z0 + zc_len);
     const int qa = max(z0 - 1, 0), qb = min(z1 + 1, nz);   // DoG planes computed
     const int len = qb - qa + KW - 1;                       // source planes loaded
     const int tlo = max(z0, 1), thi = min(z1, nz - 1);      // centre planes tested
     const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
     const uint32_t col = valid ? uint32_t(y) * uint32_t(nx) + uint32_t(x) : 0u;
     // DoG store ownership: the tile's tested columns, plus the volume's outer ring
-    const bool lastx = blockIdx.x == gridDim.x - 1, lasty = blockIdx.y == gridDim.y - 1;
-    const bool own = valid && tx >= (blockIdx.x == 0 ? 0 : 1) && (lastx || tx < kDzBX - 1) &&
-                     ty >= (blockIdx.y == 0 ? 0 : 1) && (lasty || ty < BY - 1);
+    const bool lastx = bb.bx == int(gridDim.x) - 1, lasty = bb.by == int(gridDim.y) - 1;
+    const bool own = valid && tx >= (bb.bx == 0 ? 0 : 1) && (lastx || tx < kDzBX - 1) &&
+                     ty >= (bb.by == 0 ? 0 : 1) && (lasty || ty < BY - 1);
     const bool inner = valid && tx >= 1 && tx < kDzBX - 1 && ty >= 1 && ty < BY - 1 && x <= nx - 2 &&
                        y <= ny - 2;
+    // neighbour indices clamped to the box (edge lanes are never `inner`: no branch)
+    const int xl = tx > 0 ? tx - 1 : tx, xr = tx < kDzBX - 1 ? tx + 1 : tx;
+    const int yu = ty > 0 ? ty - 1 : ty, yd = ty < BY - 1 ? ty + 1 : ty;
+    // element offset of the source plane of every window index (mirror-single
+    // extension, the tail repeating the last plane): a table read per load instead of
+    // scalar index arithmetic per unrolled step (that spilled SGPRs)
+    __shared__ uint32_t zoff[kDzMaxLen];
+    for (int i = t; i < kDzMaxLen; i += kDzBX * BY)
+        zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
     if (t < 4) nanq[t] = -1;
     __syncthreads();
-    // unconditional loads (columns outside the volume read column 0; the tail re-reads
-    // the last plane): no branch merge, so they stay in flight kDzPD planes ahead
-    auto ld = [&](int i) -> float2 {
-        return g12[uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride + col];
-    };
+    // unconditional loads (columns outside the volume read column 0): no branch merge,
+    // so they stay in flight PD planes ahead
+    auto ld = [&](int i) -> float2 { return g12[zoff[min(i, kDzMaxLen - 1)] + col]; };
     // step s: window = source planes s .. s + KW - 1 in slots (s + j) % NW, DoG plane
     // q = qa + s; the step count is padded to whole NW rotations (padded steps test and
     // store nothing), so the unrolled body has no exits
@@ -594,6 +682,12 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
     const int nsteps = (qb - qa + NW - 1) / NW * NW;
     float mnA = 0.f, mxA = 0.f, mnB = 0.f, mxB = 0.f, mnC = 0.f, mxC = 0.f, dB = 0.f, dC = 0.f;
     int nanhist = 0;   // bit k: the block's DoG plane q - k holds a NaN
+    // DoG stores: one buffer resource over the whole image with the plane in the scalar
+    // offset when the image is below 2 GiB (else one resource per plane)
+    const uint64_t dog_total = dog ? uint64_t(pstride) * uint64_t(nz) * 4u : 0u;
+    const bool one_rsrc = dog_total < 0x80000000ull;
+    const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(dog, 0, one_rsrc ? int(dog_total) : 0,
+                                                                          0x00020000);
     const uint32_t dog_bytes = dog ? pstride * 4u : 0u;
     for (int sb = 0; sb < nsteps; sb += NW) {
 #pragma unroll
@@ -610,10 +704,15 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
             const int q = qa + st;
             {   // the DoG store: a buffer store, dropped (out of range) unless owned
                 const bool st_ok = own && q >= z0 && q < z1;
-                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                    dog + (dog ? size_t(min(q, nz - 1)) * pstride : 0), 0, int(dog_bytes), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd,
-                                                      int(st_ok ? col * 4u : 0x80000000u), 0, 0);
+                const int vo = int(st_ok ? col * 4u : 0x80000000u);
+                if (one_rsrc) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
+                                                          int(uint32_t(min(q, nz - 1)) * pstride * 4u), 0);
+                } else {
+                    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                        dog + (dog ? size_t(min(q, nz - 1)) * pstride : 0), 0, int(dog_bytes), 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd, vo, 0, 0);
+                }
             }
             const int slot = q & 3;
             Dr[slot][ty][tx] = dv;
@@ -623,42 +722,26 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
             mnA = mnB; mxA = mxB; mnB = mnC; mxB = mxC;
             dB = dC;
             dC = dv;
-            if (inner) {
-                float m = dv, M = dv;
-#pragma unroll
-                for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        if (dy == 0 && dx == 0) continue;
-                        const float v = Dr[slot][ty + dy][tx + dx];
-                        m = fminf(m, v);
-                        M = fmaxf(M, v);
-                    }
-                mnC = m;
-                mxC = M;
+            {   // 3x3 box of this plane (the centre included), every lane
+                const float (*P)[kDzBX] = Dr[slot];
+                const float a0 = P[yu][xl], a1 = P[yu][tx], a2 = P[yu][xr];
+                const float b0 = P[ty][xl], b2 = P[ty][xr];
+                const float c0 = P[yd][xl], c1 = P[yd][tx], c2 = P[yd][xr];
+                mnC = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, fminf(c2, dv))));
+                mxC = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, fmaxf(c2, dv))));
             }
             const int zc = q - 1;   // centre plane of the test
             if (zc >= tlo && zc < thi) {
-                int sp = 0;
                 const float c = dB;
-                if (inner && !(fabsf(c) < pk.minv)) {
-                    bool ge, le;
-                    if (nanhist == 0) {
-                        ge = fminf(fminf(mnA, mnB), mnC) >= c;
-                        le = fmaxf(fmaxf(mxA, mxB), mxC) <= c;
-                    } else {
-                        ge = le = true;
-                        for (int dz = -1; dz <= 1; ++dz)
-                            for (int dy = -1; dy <= 1; ++dy)
-                                for (int dx = -1; dx <= 1; ++dx) {
-                                    if (dz == 0 && dy == 0 && dx == 0) continue;
-                                    const float v = Dr[(zc + dz) & 3][ty + dy][tx + dx];
-                                    ge &= v >= c;
-                                    le &= v <= c;
-                                }
-                    }
+                const bool cand = inner && !(fabsf(c) < pk.minv);
+                int sp = 0;
+                if (nanhist == 0) {
+                    const bool ge = fminf(fminf(mnA, mnB), mnC) >= c;
+                    const bool le = fmaxf(fmaxf(mxA, mxB), mxC) <= c;
                     // "this mixup is intended" (InteractiveIntegral.isSpecialPoint)
-                    sp = ge ? 2 : (le ? 1 : 0);
+                    sp = cand ? (ge ? 2 : (le ? 1 : 0)) : 0;
+                } else if (cand) {   // a NaN in the box: the reference's comparison loop
+                    sp = dz_special_nan(&Dr[0][0][0], BY, zc, ty, tx, c);
                 }
                 const bool flag = (sp == 2 && pk.want_max) || (sp == 1 && pk.want_min);
                 const unsigned long long bal = __ballot(flag);
@@ -1044,14 +1127,17 @@ int dog_env(const char* name, int def) {
     return v && *v ? std::atoi(v) : def;
 }
 
-bool is_device_ptr(const void* p) {
+// true when p is device memory of `dev` itself (read / written in place by its kernels);
+// host memory and other devices' buffers are staged through the workspace instead (a
+// kernel on dev would fault on another device's memory without peer access)
+bool is_device_ptr(const void* p, int dev) {
     if (!p) return false;
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();   // pageable host memory: not registered with HIP
         return false;
     }
-    return at.type == hipMemoryTypeDevice;
+    return at.type == hipMemoryTypeDevice && at.device == dev;
 }
 
 // Per-device DoG workspace, grown on demand and kept between calls (a 768^3 view needs
@@ -1158,9 +1244,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
 
     // the view: read in place when it already lives in HBM, else one upload
     const float* in = img;
-    if (!is_device_ptr(img)) {
+    if (!is_device_ptr(img, p->device)) {
         grow(w.in, size_t(n));
-        SD_HIP(hipMemcpyAsync(w.in.p, img, n * 4, hipMemcpyHostToDevice, s));
+        SD_HIP(hipMemcpyAsync(w.in.p, img, n * 4, hipMemcpyDefault, s));   // host or another device
         in = w.in.p;
     }
     grow(w.mm, 2 * 4096);
@@ -1178,7 +1264,7 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     }
     // DoG destination: the caller's device buffer, else the workspace (copied out at the end)
     float* dogp = nullptr;
-    const bool dog_dev = dog_out && is_device_ptr(dog_out);
+    const bool dog_dev = dog_out && is_device_ptr(dog_out, p->device);
     if (need_dog) {
         if (dog_dev) {
             dogp = dog_out;
@@ -1194,9 +1280,12 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     const int wmin = p->find_min ? 1 : 0, wmax = p->find_max ? 1 : 0;
     const bool fused = (K == 7 || K == 15 || K == 31) && n < (int64_t(1) << 32) && d.ny <= 65535 * 32 &&
                        d.nz <= 65535;
-    const int zc = std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk));
+    // (chunk + 2 + KW - 1 source planes must fit k_dog_z's kDzMaxLen plane table)
+    const int zc = std::min(kDzMaxLen - 128, std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk)));
     const int ty = dog_env("SPIMDECON_DOG_XY_TY", 48) == 32 ? 32 : 48;
     const int by = dog_env("SPIMDECON_DOG_Z_BY", 8) == 16 ? 16 : 8;
+    const int xcd = dog_env("SPIMDECON_DOG_XCD", 1);   // XCD-contiguous y-fastest boxes of k_dog_z
+    const int pd = dog_env("SPIMDECON_DOG_PD", kDzPD);  // k_dog_z planes loaded ahead (3 for A/B runs)
     const dim3 gxy(unsigned(ceil_div(d.nx, kDxyTX)), unsigned(ceil_div(d.ny, ty)), unsigned(d.nz));
     const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, kDzBX - 2))),
                   unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, by - 2))), unsigned(ceil_div(d.nz, zc)));
@@ -1204,8 +1293,8 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     if (fused) {
         grow(w.g12, size_t(n));
 #define SD_DOGXY(KV)                                                                                        \
-        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p);
+        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd);
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
@@ -1235,8 +1324,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         if (fused) {
             float* dst = store_dog ? dogp : nullptr;
 #define SD_DOGZ(KV)                                                                                          \
-            if (by == 8) hipLaunchKernelGGL((k_dog_z<KV, 8>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk); \
-            else hipLaunchKernelGGL((k_dog_z<KV, 16>), gz, dim3(kDzBX * 16), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk);
+            if (by == 16) hipLaunchKernelGGL((k_dog_z<KV, 16, kDzPD>), gz, dim3(kDzBX * 16), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd); \
+            else if (pd == 3) hipLaunchKernelGGL((k_dog_z<KV, 8, 3>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd); \
+            else hipLaunchKernelGGL((k_dog_z<KV, 8, kDzPD>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd);
             if (K == 7) { SD_DOGZ(7) } else if (K == 15) { SD_DOGZ(15) } else { SD_DOGZ(31) }
 #undef SD_DOGZ
         } else {
@@ -1265,7 +1355,7 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         SD_HIP(hipGetLastError());
         r.dpeaks = w.peaks.p;
     }
-    if (dog_out && !dog_dev) SD_HIP(hipMemcpyAsync(dog_out, dogp, n * 4, hipMemcpyDeviceToHost, s));
+    if (dog_out && !dog_dev) SD_HIP(hipMemcpyAsync(dog_out, dogp, n * 4, hipMemcpyDefault, s));
 }
 
 struct StreamHolder {

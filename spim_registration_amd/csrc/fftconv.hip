@@ -972,12 +972,26 @@ static int zdma_tx(int64_t Mz, int cz) {
 // segments) when its two buffers fit, else 16; OPT outputs per thread from the
 // instantiated set with the fewest idle output slots (nch * TR * OPT - nz), chunks of
 // H = ceil(nz / nch).  SPIMDECON_ZCHUNK=0 keeps k_zdma, =16 / =32 forces the width.
-struct ZChunk { int tx = 0, opt = 0, H = 0; };
+// SPIMDECON_ZNB=3: three buffers of 32-column tiles of OPT 8 (128-plane chunks);
+// the default keeps the two-buffer candidates below.
+struct ZChunk { int tx = 0, opt = 0, H = 0, nb = 2; };
 static ZChunk zdmc_plan(int64_t nz, int KC) {
     const char* e = std::getenv("SPIMDECON_ZCHUNK");
     const int force = e ? std::atoi(e) : -1;
+    const char* enb = std::getenv("SPIMDECON_ZNB");
+    const int nb = enb && std::atoi(enb) == 3 ? 3 : 2;   // 3 buffers measured slower (0.318 vs 0.273 ms)
     ZChunk best;
     if (force == 0 || KC == 0 || nz < 1) return best;
+    if (force == 64) {   // 64-column tiles: 512-B plane segments (A/B runs)
+        const int opt = KC == 16 ? 8 : 12;
+        const int64_t nch = ceil_div(nz, int64_t(kZdThreads / 64) * opt);
+        return {64, opt, int(ceil_div(nz, nch)), 2};
+    }
+    if (nb == 3 && force != 16) {
+        const int64_t nch = ceil_div(nz, int64_t(kZdThreads / 32) * 8);
+        best = {32, 8, int(ceil_div(nz, nch)), 3};
+        return best;
+    }
     struct Cand { int tx, opt; };
     std::vector<Cand> cands;
     if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
@@ -990,7 +1004,7 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
         const int64_t nch = ceil_div(nz, cap);
         const int64_t waste = nch * cap - nz;
         if (bw < 0 || waste < bw) {
-            best = {c.tx, c.opt, int(ceil_div(nz, nch))};
+            best = {c.tx, c.opt, int(ceil_div(nz, nch)), 2};
             bw = waste;
         }
     }
@@ -1031,19 +1045,20 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
         const float kscale = float(p.g.Mz);
         bool done = false;
-#define SD_ZC(KCV, OPTV, TXV)                                                                           \
-        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV)) {                               \
-            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV));                                         \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV>),          \
+#define SD_ZC(KCV, OPTV, TXV, NBV)                                                                      \
+        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV)) {             \
+            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV));                                    \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>),     \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
-            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, C, \
-                               Kc, p.g.cz, zc.H, bytes, kscale);                                        \
+            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, \
+                               C, Kc, p.g.cz, zc.H, bytes, kscale);                                     \
             done = true;                                                                                \
         }
-#define SD_ZC4(KCV) SD_ZC(KCV, 16, 32) SD_ZC(KCV, 12, 32) SD_ZC(KCV, 8, 32) SD_ZC(KCV, 17, 16) \
-        SD_ZC(KCV, 13, 16) SD_ZC(KCV, 9, 16)
+#define SD_ZC4(KCV) SD_ZC(KCV, 16, 32, 2) SD_ZC(KCV, 12, 32, 2) SD_ZC(KCV, 8, 32, 2) SD_ZC(KCV, 17, 16, 2) \
+        SD_ZC(KCV, 13, 16, 2) SD_ZC(KCV, 9, 16, 2) SD_ZC(KCV, 8, 32, 3) SD_ZC(KCV, 12, 64, 2)
         SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
-        SD_ZC(16, 15, 32) SD_ZC(16, 12, 32) SD_ZC(16, 8, 32) SD_ZC(16, 17, 16) SD_ZC(16, 13, 16) SD_ZC(16, 9, 16)
+        SD_ZC(16, 15, 32, 2) SD_ZC(16, 12, 32, 2) SD_ZC(16, 8, 32, 2) SD_ZC(16, 17, 16, 2) SD_ZC(16, 13, 16, 2)
+        SD_ZC(16, 9, 16, 2) SD_ZC(16, 8, 32, 3) SD_ZC(16, 8, 64, 2)
 #undef SD_ZC4
 #undef SD_ZC
         SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");

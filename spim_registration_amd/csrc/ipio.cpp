@@ -124,7 +124,8 @@ void load_interest_points(const char* base_dir, const char* file, spim_interest_
     SD_CHECK(nout, SPIMDECON_ERR_ARG, "null count");
     const std::string path = ip_path(base_dir, file);
     FILE* f = std::fopen(path.c_str(), "r");
-    SD_CHECK(f, SPIMDECON_ERR_ARG, "cannot read " + path + ": " + std::strerror(errno));
+    // an IOException: loadInterestPoints prints it and returns false (:209-214)
+    SD_CHECK(f, SPIMDECON_ERR_IO, "cannot read " + path + ": " + std::strerror(errno));
     std::vector<char> line(1 << 16);
     bool header = false;
     int64_t n = 0;
@@ -135,14 +136,25 @@ void load_interest_points(const char* base_dir, const char* file, spim_interest_
         }
         char* s = line.data();
         if (*s == '\n' || *s == 0) continue;
+        // fields split at '\t' and trimmed, as Integer.parseInt(p[0].trim()) /
+        // Double.parseDouble(p[d].trim()) (:194-199): strtol / strtod skip the leading
+        // blanks, skip_blanks the trailing ones
+        auto skip_blanks = [](char* q) {
+            while (*q == ' ' || *q == '\r' || *q == '\f' || *q == '\v') ++q;
+            return q;
+        };
         char* e = nullptr;
         const long id = std::strtol(s, &e, 10);
         double pos[3];
-        bool ok = e != s && *e == '\t';
+        bool ok = e != s && *(e = skip_blanks(e)) == '\t';
         for (int d = 0; d < 3 && ok; ++d) {
             s = e + 1;
             pos[d] = std::strtod(s, &e);
-            ok = e != s && (d == 2 || *e == '\t');
+            ok = e != s;
+            if (ok) {
+                e = skip_blanks(e);
+                ok = d == 2 ? (*e == '\t' || *e == '\n' || *e == 0) : *e == '\t';
+            }
         }
         if (!ok) {
             std::fclose(f);

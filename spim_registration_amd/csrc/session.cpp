@@ -268,6 +268,12 @@ void Session::add_view(const float* img, const float* weight, const float* k1, c
     hk.data.assign(k1, k1 + int64_t(kdims[0]) * kdims[1] * kdims[2]);
     // device pointers live on the first device; other groups copy them peer to peer
     const hipMemcpyKind kind = device_ptrs ? hipMemcpyDefault : hipMemcpyHostToDevice;
+    if (device_ptrs) {
+        // the caller may still be writing them on another stream (torch's default stream
+        // does not order against the session's non-blocking streams): wait for the device
+        DeviceGuard guard(p_.device);
+        SD_HIP(hipDeviceSynchronize());
+    }
     std::vector<std::vector<DBuf<char>>> bufs(slabs_.size());
     for (auto& gr : groups_) {
         DeviceGuard guard(gr.dev);

@@ -28,14 +28,18 @@ class InterestPoint:
 def compute(img: np.ndarray, sigma: float = 1.8, threshold: float = 0.008, localization: int = 0,
             image_sigma=(0.5, 0.5, 0.5), find_min: bool = False, find_max: bool = True,
             min_intensity: float = float("nan"), max_intensity: float = float("nan"),
-            keep_intensity: bool = False, device: int = 0, ij_threads: int = 8,
+            keep_intensity: bool = False, device: int | None = None, ij_threads: int = 8,
             return_dog: bool = False, max_peaks: int | None = None):
     """ProcessDOG.compute: returns the list of InterestPoint (and the DoG image
     when ``return_dog``).  ``img`` is a [z, y, x] float32 volume (not modified):
     a numpy array, or a torch tensor on the GPU -- a view already resident in HBM
-    is read in place (the returned DoG image is then a torch tensor too)."""
+    is read in place (the returned DoG image is then a torch tensor too).
+    ``device``: the GPU that runs the pass; default the tensor's own GPU (device 0 for
+    a host array)."""
     lib = _lib.load()
     on_dev = hasattr(img, "is_cuda") and img.is_cuda
+    if device is None:
+        device = img.device.index if on_dev else 0
     if on_dev:
         img = img.contiguous().float()
         if img.dim() != 3:
@@ -131,10 +135,13 @@ def _compute_device(lib, img, sigma, threshold, localization, image_sigma, find_
 def interest_points_array(img, sigma: float = 1.8, threshold: float = 0.008, localization: int = 0,
                           image_sigma=(0.5, 0.5, 0.5), find_min: bool = False, find_max: bool = True,
                           min_intensity: float = float("nan"), max_intensity: float = float("nan"),
-                          device: int = 0, ij_threads: int = 8):
+                          device: int | None = None, ij_threads: int = 8):
     """ProcessDOG.compute on a GPU tensor, as arrays: (positions (n, 3) x, y, z;
-    intensities (n,)) in the reference's order -- no per-point Python objects."""
+    intensities (n,)) in the reference's order -- no per-point Python objects.
+    ``device`` defaults to the tensor's own GPU."""
     lib = _lib.load()
+    if device is None:
+        device = img.device.index
     img = img.contiguous().float()
     p = _params(lib, sigma, threshold, localization, image_sigma, find_min, find_max, min_intensity,
                 max_intensity, device, ij_threads)
@@ -207,11 +214,15 @@ class InterestPointList:
         return True
 
     def load_interest_points(self) -> bool:
-        """loadInterestPoints (:178-220)."""
+        """loadInterestPoints (:178-220): False when the file cannot be read (the
+        reference catches the IOException); a malformed line raises (Java's
+        NumberFormatException is not caught there either)."""
         lib = _lib.load()
         n = C.c_int64(0)
-        check(lib.spim_load_interest_points(self.base_dir.encode(), self.file.encode(), None, None, 0,
-                                            C.byref(n)))
+        st = lib.spim_load_interest_points(self.base_dir.encode(), self.file.encode(), None, None, 0, C.byref(n))
+        if st == _lib.ERR_IO:
+            return False
+        check(st)
         cap = max(int(n.value), 1)
         arr = (_lib.InterestPointC * cap)()
         ids = (C.c_int32 * cap)()

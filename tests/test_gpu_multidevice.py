@@ -208,3 +208,18 @@ def test_c3_strong_decomposition_exchange_accounting(gpu):
         assert tm[8 + 5] == 2 * iters * V               # group 0's exchange intervals
         print(f"\nC3 8-group exchange: {plane * cz / 1e6:.1f} MB per copy, {(b1 - b0) / iters / 1e9:.2f} GB "
               f"per iteration (all boundaries), {tm[5] / tm[13]:.3f} ms per exchange on group 0's stream")
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() < 2, reason="needs 2 distinct GPUs (the pool's boxes have 1)")
+def test_distinct_devices_match_single(gpu):
+    """Peer pulls over xGMI between distinct GPUs: the same psi and stats as one
+    device (runs wherever >= 2 GPUs are visible, e.g. the 8-GPU node; on one GPU the
+    same code path is covered by the repeated-id tests above)."""
+    import torch
+    n = min(torch.cuda.device_count(), 4)
+    imgs, ws, ks, _ = tile_case(V=3, cid=15)
+    psi1, st1, _, _, _ = run_session(imgs, ws, ks)
+    psi, st, modes, ndev, devs = run_session(imgs, ws, ks, devices=list(range(n)))
+    assert ndev == n and devs == list(range(n))
+    assert rel_l2(psi, psi1) < 1e-5
+    np.testing.assert_allclose(st, st1, rtol=1e-4)

@@ -59,8 +59,20 @@ def test_load_skips_preamble_and_keeps_ids(lib, tmp_path):
     ipl = InterestPointList(str(tmp_path), "x")
     assert ipl.load_interest_points()
     assert [(p.id, p.location) for p in ipl.get_interest_points()] == [(7, (1.0, 2.5, 3e-4)), (9, (4.0, 5.0, 6.0))]
+    # a missing file is the reference's caught IOException: false, no exception (:209-214)
+    assert InterestPointList(str(tmp_path), "missing").load_interest_points() is False
+
+
+def test_load_trims_fields_like_java(lib, tmp_path):
+    """p[i].trim() before parseInt / parseDouble (InterestPointList.java:194-199): blanks
+    around every tab-separated field are accepted; a non-number still raises."""
+    (tmp_path / "w.ip.txt").write_text("id\tx\ty\tz\n 3 \t 1.5 \t2.0 \t 4.25 \r\n4\t0.5\t0.25\t1.0E1\n")
+    ipl = InterestPointList(str(tmp_path), "w")
+    assert ipl.load_interest_points()
+    assert [(p.id, p.location) for p in ipl.get_interest_points()] == [(3, (1.5, 2.0, 4.25)), (4, (0.5, 0.25, 10.0))]
+    (tmp_path / "bad.ip.txt").write_text("id\tx\ty\tz\n3\tabc\t2.0\t4.0\n")
     with pytest.raises(_lib.SpimDeconError):
-        InterestPointList(str(tmp_path), "missing").load_interest_points()
+        InterestPointList(str(tmp_path), "bad").load_interest_points()
 
 
 def test_convolution_cpu_has_no_cpu_path(lib):

@@ -11,11 +11,12 @@ for v in "$@"; do
   env $v true || exit 1
   (export $v; timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/v$i -o k --output-format csv -- python3 tools/dog_bench.py --reps 3 --device-only > $OUT/v$i.log 2>&1) || exit $?
   echo "== v$i: $v" >> $OUT/summary.txt
-  tail -1 $OUT/v$i.log >> $OUT/summary.txt
+  grep '^{' $OUT/v$i.log | tail -1 >> $OUT/summary.txt
   python3 - $OUT/v$i/k_kernel_stats.csv >> $OUT/summary.txt <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
     if "k_dog" in r["Name"] or "k_minmax(" in r["Name"]:
-        print(f'  {__import__("re").search(r"(k_\w+(<[^>]*>)?)", r["Name"]).group(1):40s} max {float(r["MaxNs"])/1e3:8.1f} us  min {float(r["MinNs"])/1e3:8.1f} us')
+        name = r["Name"].split("::")[-1][:48]
+        print("  %-48s max %8.1f us  avg %8.1f us" % (name, float(r["MaxNs"]) / 1e3, float(r["AverageNs"]) / 1e3))
 PY
 done
