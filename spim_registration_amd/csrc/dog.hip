@@ -358,7 +358,7 @@ constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave pe
                              // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
 constexpr int kDzPD = 8;     // planes loaded ahead of use: 3 left the HBM latency exposed
                              // (a step computes in ~350 cycles; a load takes thousands)
-constexpr int kDzChunk = 64; // DoG planes per block (the window adds KW - 1 + 2 loads)
+constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
 constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
 
 __device__ __forceinline__ int mirror32(int i, int n) {
@@ -389,9 +389,9 @@ constexpr int kDxySxP = kDxyTX + 2;
 // (Markstein's theorem; the Tikhonov step, rl_math.hpp, uses the same scheme in double).
 // Outside the range where the residuals are exact (0, tiny, huge or non-finite a) the
 // IEEE division itself.  5 VALU instead of the ~10 of the scaled division sequence.
-__device__ __forceinline__ float div_rn_rcp(float a, float diff, float rd) {
-    const float aa = fabsf(a);
-    if (!(aa >= 0x1p-48f && aa <= 0x1p48f)) return __fdiv_rn(a, diff);   // q and residuals stay normal
+// (caller: |a| in [2^-48, 2^48] or a == +0, and diff in [2^-48, 2^48]: q and the
+// residuals stay normal; -0 would come out +0, so it takes the division)
+__device__ __forceinline__ float div_rn_rcp_core(float a, float diff, float rd) {
     float q = __fmul_rn(a, rd);
     q = __fmaf_rn(__fmaf_rn(-q, diff, a), rd, q);
     return __fmaf_rn(__fmaf_rn(-q, diff, a), rd, q);
@@ -469,14 +469,30 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
             v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
         }
     }
+    if (norm) {
+        // one wave-uniform decision for all NE values: the reciprocal path unless a value
+        // of the wave leaves its exact range (then the IEEE division for all of them)
+        bool bad = rd == 0.0f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            v[e] = __fsub_rn(v[e], mn);
+            const float aa = fabsf(v[e]);
+            bad |= !((aa >= 0x1p-48f && aa <= 0x1p48f) || __float_as_uint(v[e]) == 0u);   // (+0 only)
+        }
+        if (!__any(bad)) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
+        } else {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) v[e] = __fdiv_rn(v[e], diff);
+        }
+    }
     if (cact) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int row = r0 + RPT * e;
             if (row >= IH) break;
-            sin_[row * IP + col] = norm ? (rd != 0.0f ? div_rn_rcp(__fsub_rn(v[e], mn), diff, rd)
-                                                      : __fdiv_rn(__fsub_rn(v[e], mn), diff))
-                                        : v[e];
+            sin_[row * IP + col] = v[e];
         }
     }
     __syncthreads();

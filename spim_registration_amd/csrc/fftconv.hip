@@ -1044,6 +1044,10 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256));
         const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
         const float kscale = float(p.g.Mz);
+        static const int sgrp = [] {   // blocks sharing a plane order (SPIMDECON_ZSTAG_GROUP, A/B)
+            const char* e = std::getenv("SPIMDECON_ZSTAG_GROUP");
+            return e ? std::max(1, std::atoi(e)) : 1;
+        }();
         bool done = false;
 #define SD_ZC(KCV, OPTV, TXV, NBV)                                                                      \
         if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV)) {             \
@@ -1051,7 +1055,7 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
             SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>),     \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
             hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, \
-                               C, Kc, p.g.cz, zc.H, bytes, kscale);                                     \
+                               C, Kc, p.g.cz, zc.H, bytes, kscale, sgrp);                               \
             done = true;                                                                                \
         }
 #define SD_ZC4(KCV) SD_ZC(KCV, 16, 32, 2) SD_ZC(KCV, 12, 32, 2) SD_ZC(KCV, 8, 32, 2) SD_ZC(KCV, 17, 16, 2) \
