@@ -431,10 +431,10 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     __shared__ __attribute__((aligned(16))) float sin_[IH * IP];
     __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxySxP];
     const int nx = int(d.nx), ny = int(d.ny);
-    const DzBox bb = xcd_box<false>(xcd != 0);
-    const int x0 = bb.bx * kDxyTX, y0 = bb.by * TY;
-    const uint32_t plane = uint32_t(bb.bz) * uint32_t(ny) * uint32_t(nx);
+    const int gx = (nx + kDxyTX - 1) / kDxyTX, gy = (ny + TY - 1) / TY;
+    const int ntiles = gx * gy * int(d.nz);
     const int t = threadIdx.x;
+    (void)xcd;
     // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
     bool norm = false;
     float mn = 0.0f, diff = 1.0f, rd = 1.0f;
@@ -447,101 +447,122 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     }
     // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
     // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
-    // load; every load in flight before the first use (a load per round trip exposed
-    // the HBM latency ~19 times per tile).  Tiles whose staged box lies inside the
-    // volume (all but the outer ring of tiles) index without the mirror arithmetic.
+    // load.  Tiles whose staged box lies inside the volume (all but the outer ring of
+    // tiles) index without the mirror arithmetic.
     constexpr int RPT = 256 / IW;                // rows staged per pass
     constexpr int IPC = 256 / RPT;               // threads per row (>= IW)
     constexpr int NE = (IH + RPT - 1) / RPT;     // rows per thread
     const int col = t % IPC, r0 = t / IPC;
     const bool cact = col < IW && r0 < RPT;
-    const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && y0 - R >= 0 && y0 - R + IH <= ny;
-    float v[NE];
-    if (inside) {
-        const uint32_t base = plane + uint32_t(y0 - R) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
+    auto tile_xyz = [&](int tile, int& x0, int& y0, uint32_t& plane) {   // x fastest, then y, then z
+        x0 = (tile % gx) * kDxyTX;
+        y0 = ((tile / gx) % gy) * TY;
+        plane = uint32_t(tile / (gx * gy)) * uint32_t(ny) * uint32_t(nx);
+    };
+    auto stage_loads = [&](int tile, float* v) {
+        int x0, y0;
+        uint32_t plane;
+        tile_xyz(tile, x0, y0, plane);
+        const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && y0 - R >= 0 && y0 - R + IH <= ny;
+        if (inside) {
+            const uint32_t base = plane + uint32_t(y0 - R) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
 #pragma unroll
-        for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
-    } else {
-        const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int row = min(r0 + RPT * e, IH - 1);
-            v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
-        }
-    }
-    if (norm) {
-        // one wave-uniform decision for all NE values: the reciprocal path unless a value
-        // of the wave leaves its exact range (then the IEEE division for all of them)
-        bool bad = rd == 0.0f;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            v[e] = __fsub_rn(v[e], mn);
-            const float aa = fabsf(v[e]);
-            bad |= !((aa >= 0x1p-48f && aa <= 0x1p48f) || __float_as_uint(v[e]) == 0u);   // (+0 only)
-        }
-        if (!__any(bad)) {
-#pragma unroll
-            for (int e = 0; e < NE; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
+            for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
         } else {
+            const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
 #pragma unroll
-            for (int e = 0; e < NE; ++e) v[e] = __fdiv_rn(v[e], diff);
+            for (int e = 0; e < NE; ++e) {
+                const int row = min(r0 + RPT * e, IH - 1);
+                v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
+            }
         }
-    }
-    if (cact) {
+    };
+    // persistent blocks: the next tile's input values are loaded into registers while
+    // this tile is transformed (one tile per block exposed the HBM latency of staging)
+    float v[NE];
+    int tile = blockIdx.x;
+    if (tile < ntiles) stage_loads(tile, v);
+    for (; tile < ntiles; tile += gridDim.x) {
+        int x0, y0;
+        uint32_t plane;
+        tile_xyz(tile, x0, y0, plane);
+        if (norm) {
+            // one wave-uniform decision for all NE values: the reciprocal path unless a
+            // value of the wave leaves its exact range (then the IEEE division for all)
+            bool bad = rd == 0.0f;
 #pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int row = r0 + RPT * e;
-            if (row >= IH) break;
-            sin_[row * IP + col] = v[e];
+            for (int e = 0; e < NE; ++e) {
+                v[e] = __fsub_rn(v[e], mn);
+                const float aa = fabsf(v[e]);
+                bad |= !((aa >= 0x1p-48f && aa <= 0x1p48f) || __float_as_uint(v[e]) == 0u);   // (+0 only)
+            }
+            if (!__any(bad)) {
+#pragma unroll
+                for (int e = 0; e < NE; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
+            } else {
+#pragma unroll
+                for (int e = 0; e < NE; ++e) v[e] = __fdiv_rn(v[e], diff);
+            }
         }
-    }
-    __syncthreads();
-    // x phase: lane = staged row, the wave's segment of kDxySeg outputs from a window of
-    // WX values (b128 reads conflict-free through the pitch IP)
-    for (int it = t; it < IHP * NSEG; it += 256) {
-        const int row = it % IHP, seg = it / IHP;
-        if (row >= IH) continue;
-        const float* src = sin_ + row * IP + seg * kDxySeg;
-        float w[WX];
+        if (cact) {   // (the previous tile's x phase finished at its mid-tile barrier)
 #pragma unroll
-        for (int i = 0; i < WX; ++i) w[i] = src[i];
-        dg_v2 acc[kDxySeg];
-#pragma unroll
-        for (int o = 0; o < kDxySeg; ++o) acc[o] = dg_v2{0.0f, 0.0f};
-#pragma unroll
-        for (int j = 0; j < KW; ++j) {
-            const dg_v2 k = dg_v2{kx[j].x, kx[j].y};
-#pragma unroll
-            for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
+            for (int e = 0; e < NE; ++e) {
+                const int row = r0 + RPT * e;
+                if (row >= IH) break;
+                sin_[row * IP + col] = v[e];
+            }
         }
-        float2* dst = sx + row * kDxySxP + seg * kDxySeg;
+        const int next = tile + int(gridDim.x);
+        if (next < ntiles) stage_loads(next, v);   // in flight during this tile's phases
+        __syncthreads();   // (also: the previous tile's y phase no longer reads sx)
+        // x phase: lane = staged row, the wave's segment of kDxySeg outputs from a window
+        // of WX values (b128 reads conflict-free through the pitch IP)
+        for (int it = t; it < IHP * NSEG; it += 256) {
+            const int row = it % IHP, seg = it / IHP;
+            if (row >= IH) continue;
+            const float* src = sin_ + row * IP + seg * kDxySeg;
+            float w[WX];
 #pragma unroll
-        for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
-    }
-    __syncthreads();
-    // y phase: column c, OY consecutive outputs
-    const int c = t & (kDxyTX - 1), run = t / kDxyTX;
-    const int x = x0 + c;
-    if (x >= nx) return;
-    dg_v2 w[WY];
+            for (int i = 0; i < WX; ++i) w[i] = src[i];
+            dg_v2 acc[kDxySeg];
 #pragma unroll
-    for (int i = 0; i < WY; ++i) {
-        const float2 v = sx[(run * OY + i) * kDxySxP + c];
-        w[i] = dg_v2{v.x, v.y};
-    }
-    dg_v2 acc[OY];
+            for (int o = 0; o < kDxySeg; ++o) acc[o] = dg_v2{0.0f, 0.0f};
 #pragma unroll
-    for (int o = 0; o < OY; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+            for (int j = 0; j < KW; ++j) {
+                const dg_v2 k = dg_v2{kx[j].x, kx[j].y};
 #pragma unroll
-    for (int j = 0; j < KW; ++j) {
-        const dg_v2 k = dg_v2{ky[j].x, ky[j].y};
+                for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
+            }
+            float2* dst = sx + row * kDxySxP + seg * kDxySeg;
 #pragma unroll
-        for (int o = 0; o < OY; ++o) acc[o] = acc[o] + w[o + j] * k;
-    }
+            for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
+        }
+        __syncthreads();
+        // y phase: column c, OY consecutive outputs
+        const int c = t & (kDxyTX - 1), run = t / kDxyTX;
+        const int x = x0 + c;
+        if (x < nx) {
+            dg_v2 w[WY];
 #pragma unroll
-    for (int o = 0; o < OY; ++o) {
-        const int y = y0 + run * OY + o;
-        if (y < ny) g12[plane + uint32_t(y) * uint32_t(nx) + uint32_t(x)] = make_float2(acc[o].x, acc[o].y);
+            for (int i = 0; i < WY; ++i) {
+                const float2 vv = sx[(run * OY + i) * kDxySxP + c];
+                w[i] = dg_v2{vv.x, vv.y};
+            }
+            dg_v2 acc[OY];
+#pragma unroll
+            for (int o = 0; o < OY; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const dg_v2 k = dg_v2{ky[j].x, ky[j].y};
+#pragma unroll
+                for (int o = 0; o < OY; ++o) acc[o] = acc[o] + w[o + j] * k;
+            }
+#pragma unroll
+            for (int o = 0; o < OY; ++o) {
+                const int y = y0 + run * OY + o;
+                if (y < ny) g12[plane + uint32_t(y) * uint32_t(nx) + uint32_t(x)] = make_float2(acc[o].x, acc[o].y);
+            }
+        }
     }
 }
 
@@ -597,9 +618,13 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void cand_flush(const PeakSink& pk, const int4* buf, int n, int nx, uint32_t pstride) {
+// (the sink is read through a pointer: its fields are loaded here, at a flush, instead of
+// holding 10 SGPRs for the whole z loop)
+__device__ __forceinline__ void cand_flush(const PeakSink* __restrict__ sink, const int4* buf, int n, int nx,
+                                           uint32_t pstride) {
     if (n == 0) return;
     wave_lds_sync();
+    const PeakSink pk = *sink;
     const int lane = int(threadIdx.x & 63);
     unsigned base = 0;
     if (lane == 0) base = atomicAdd(pk.count, unsigned(n));
@@ -630,37 +655,46 @@ __device__ __forceinline__ void cand_flush(const PeakSink& pk, const int4* buf, 
 // 26-neighbour test is min / max of the 3x3x3 box (the box includes the centre, so
 // "all neighbours >= c" <=> box min >= c); a plane holding a NaN takes the
 // reference's comparison loop instead (NaN compares false).
-// InteractiveIntegral.isSpecialPoint (:443-468) over the 4-plane ring Dr[4][by][kDzBX]
+// InteractiveIntegral.isSpecialPoint (:443-468) over the 4-plane ring Dr[4][by][BX]
 // (centre plane zc, row ty, column tx): 2 = every neighbour >= c ("MAX"), 1 = every
 // neighbour <= c, 0 = neither.  Only for boxes holding a NaN (compares false), out of
 // line: the min / max test covers every other box.
-__device__ __noinline__ int dz_special_nan(const float* Dr, int by, int zc, int ty, int tx, float c) {
+__device__ __noinline__ int dz_special_nan(const float* Dr, int by, int bx, int zc, int ty, int tx, float c) {
     bool ge = true, le = true;
     for (int dz = -1; dz <= 1; ++dz)
         for (int dy = -1; dy <= 1; ++dy)
             for (int dx = -1; dx <= 1; ++dx) {
                 if (dz == 0 && dy == 0 && dx == 0) continue;
-                const float v = Dr[(((zc + dz) & 3) * by + ty + dy) * kDzBX + tx + dx];
+                const float v = Dr[(((zc + dz) & 3) * by + ty + dy) * bx + tx + dx];
                 ge &= v >= c;
                 le &= v <= c;
             }
     return ge ? 2 : (le ? 1 : 0);
 }
 
-template <int KW, int BY, int PD>
-__global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
+// BX x BY columns per block (BX * BY = 512 threads): 64 x 8 = one wave per row, or 32 x
+// 16 = two rows per wave -- fewer recomputed halo columns (32 x 16 tests 30 x 14 of 512
+// columns, 64 x 8 only 62 x 6)
+// ONE: the DoG image is below 2 GiB, one buffer resource covers it (the plane goes in
+// the scalar offset); else a resource per plane.  want: bit 0 minima, bit 1 maxima.
+// The z taps are symmetric (gaussian_kernel builds them so): taps j and KW - 1 - j are
+// the same value and only R + 1 of them are held in SGPRs.
+template <int KW, int BY, int PD, int BX, bool ONE>
+__global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
                                                          const float2* __restrict__ kz, float scale, int zc_len,
-                                                         float* __restrict__ dog, PeakSink pk, int xcd) {
+                                                         float* __restrict__ dog, float minv, int want,
+                                                         const PeakSink* __restrict__ sink, int xcd) {
     constexpr int R = KW / 2;
     constexpr int NW = KW + PD;
-    __shared__ float Dr[4][BY][kDzBX];
+    __shared__ float Dr[4][BY][BX];
     __shared__ int nanq[4];
-    __shared__ int4 cbuf[BY][kCandBuf];   // one candidate buffer per wave (= row ty)
+    __shared__ int4 cbuf[BX * BY / 64][kCandBuf];   // one candidate buffer per wave
     int ccount = 0;                       // wave-uniform fill of this wave's buffer
-    const int t = threadIdx.x, tx = t & (kDzBX - 1), ty = t / kDzBX;
+    const int t = threadIdx.x, tx = t & (BX - 1), ty = t / BX;
+    const int wv = t >> 6, lane = t & 63;
     const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
     const DzBox bb = xcd_box<true>(xcd != 0);
-    const int X0 = bb.bx * (kDzBX - 2), Y0 = bb.by * (BY - 2);
+    const int X0 = bb.bx * (BX - 2), Y0 = bb.by * (BY - 2);
     const int x = X0 + tx, y = Y0 + ty;
     const bool valid = x < nx && y < ny;
     const int z0 = bb.bz * zc_len, z1 = min(nz, z0 + zc_len);
@@ -671,18 +705,18 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
     const uint32_t col = valid ? uint32_t(y) * uint32_t(nx) + uint32_t(x) : 0u;
     // DoG store ownership: the tile's tested columns, plus the volume's outer ring
     const bool lastx = bb.bx == int(gridDim.x) - 1, lasty = bb.by == int(gridDim.y) - 1;
-    const bool own = valid && tx >= (bb.bx == 0 ? 0 : 1) && (lastx || tx < kDzBX - 1) &&
+    const bool own = valid && tx >= (bb.bx == 0 ? 0 : 1) && (lastx || tx < BX - 1) &&
                      ty >= (bb.by == 0 ? 0 : 1) && (lasty || ty < BY - 1);
-    const bool inner = valid && tx >= 1 && tx < kDzBX - 1 && ty >= 1 && ty < BY - 1 && x <= nx - 2 &&
+    const bool inner = valid && tx >= 1 && tx < BX - 1 && ty >= 1 && ty < BY - 1 && x <= nx - 2 &&
                        y <= ny - 2;
     // neighbour indices clamped to the box (edge lanes are never `inner`: no branch)
-    const int xl = tx > 0 ? tx - 1 : tx, xr = tx < kDzBX - 1 ? tx + 1 : tx;
+    const int xl = tx > 0 ? tx - 1 : tx, xr = tx < BX - 1 ? tx + 1 : tx;
     const int yu = ty > 0 ? ty - 1 : ty, yd = ty < BY - 1 ? ty + 1 : ty;
     // element offset of the source plane of every window index (mirror-single
     // extension, the tail repeating the last plane): a table read per load instead of
     // scalar index arithmetic per unrolled step (that spilled SGPRs)
     __shared__ uint32_t zoff[kDzMaxLen];
-    for (int i = t; i < kDzMaxLen; i += kDzBX * BY)
+    for (int i = t; i < kDzMaxLen; i += BX * BY)
         zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
     if (t < 4) nanq[t] = -1;
     __syncthreads();
@@ -701,10 +735,10 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
     // DoG stores: one buffer resource over the whole image with the plane in the scalar
     // offset when the image is below 2 GiB (else one resource per plane)
     const uint64_t dog_total = dog ? uint64_t(pstride) * uint64_t(nz) * 4u : 0u;
-    const bool one_rsrc = dog_total < 0x80000000ull;
-    const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(dog, 0, one_rsrc ? int(dog_total) : 0,
+    const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(dog, 0, ONE ? int(dog_total) : 0,
                                                                           0x00020000);
     const uint32_t dog_bytes = dog ? pstride * 4u : 0u;
+    const bool want_min = (want & 1) != 0, want_max = (want & 2) != 0;
     for (int sb = 0; sb < nsteps; sb += NW) {
 #pragma unroll
         for (int ph = 0; ph < NW; ++ph) {
@@ -714,14 +748,15 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
 #pragma unroll
             for (int j = 0; j < KW; ++j) {   // tap order kept
                 const float2 v = w[(ph + j) % NW];
-                acc = acc + dg_v2{v.x, v.y} * dg_v2{kz[j].x, kz[j].y};
+                const float2 k = kz[j <= R ? j : KW - 1 - j];
+                acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
             }
             const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
             const int q = qa + st;
             {   // the DoG store: a buffer store, dropped (out of range) unless owned
                 const bool st_ok = own && q >= z0 && q < z1;
                 const int vo = int(st_ok ? col * 4u : 0x80000000u);
-                if (one_rsrc) {
+                if constexpr (ONE) {
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
                                                           int(uint32_t(min(q, nz - 1)) * pstride * 4u), 0);
                 } else {
@@ -739,7 +774,7 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
             dB = dC;
             dC = dv;
             {   // 3x3 box of this plane (the centre included), every lane
-                const float (*P)[kDzBX] = Dr[slot];
+                const float (*P)[BX] = Dr[slot];
                 const float a0 = P[yu][xl], a1 = P[yu][tx], a2 = P[yu][xr];
                 const float b0 = P[ty][xl], b2 = P[ty][xr];
                 const float c0 = P[yd][xl], c1 = P[yd][tx], c2 = P[yd][xr];
@@ -749,7 +784,7 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
             const int zc = q - 1;   // centre plane of the test
             if (zc >= tlo && zc < thi) {
                 const float c = dB;
-                const bool cand = inner && !(fabsf(c) < pk.minv);
+                const bool cand = inner && !(fabsf(c) < minv);
                 int sp = 0;
                 if (nanhist == 0) {
                     const bool ge = fminf(fminf(mnA, mnB), mnC) >= c;
@@ -757,25 +792,25 @@ __global__ __launch_bounds__(kDzBX * BY) void k_dog_z(Dims3 d, const float2* __r
                     // "this mixup is intended" (InteractiveIntegral.isSpecialPoint)
                     sp = cand ? (ge ? 2 : (le ? 1 : 0)) : 0;
                 } else if (cand) {   // a NaN in the box: the reference's comparison loop
-                    sp = dz_special_nan(&Dr[0][0][0], BY, zc, ty, tx, c);
+                    sp = dz_special_nan(&Dr[0][0][0], BY, BX, zc, ty, tx, c);
                 }
-                const bool flag = (sp == 2 && pk.want_max) || (sp == 1 && pk.want_min);
+                const bool flag = (sp == 2 && want_max) || (sp == 1 && want_min);
                 const unsigned long long bal = __ballot(flag);
                 if (bal != 0ull) {
                     const int nb = __popcll(bal);
                     if (ccount + nb > kCandBuf) {
-                        cand_flush(pk, cbuf[ty], ccount, nx, pstride);
+                        cand_flush(sink, cbuf[wv], ccount, nx, pstride);
                         ccount = 0;
                     }
                     if (flag)
-                        cbuf[ty][ccount + __popcll(bal & ((1ull << (tx & 63)) - 1ull))] =
+                        cbuf[wv][ccount + __popcll(bal & ((1ull << lane) - 1ull))] =
                             make_int4(x, y | (sp << 30), zc, __float_as_int(fabsf(c)));
                     ccount += nb;
                 }
             }
         }
     }
-    cand_flush(pk, cbuf[ty], ccount, nx, pstride);
+    cand_flush(sink, cbuf[wv], ccount, nx, pstride);
 }
 
 __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in, int64_t n,
@@ -1173,12 +1208,14 @@ struct DogWork {
     DBuf<spim_interest_point> ips, ips_sel;  // interest points before / after the threshold
     DBuf<unsigned char> flags, sel_tmp;
     DBuf<int> nsel;
+    DBuf<PeakSink> sink;                   // k_dog_z's sink, read at its flushes
     void release() {
         for (DBuf<float>* b : {&in, &dog, &taps, &mm, &tmp_a, &tmp_b, &tmp_c, &tmp_d}) b->release();
         g12.release();
         keys.release(); keys_sorted.release(); vals.release(); vals_sorted.release();
         recs.release(); peaks.release(); count.release(); sort_tmp.release();
         loc.release(); ips.release(); ips_sel.release(); flags.release(); sel_tmp.release(); nsel.release();
+        sink.release();
     }
 };
 
@@ -1248,6 +1285,10 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         kall.insert(kall.end(), k2[a].begin(), k2[a].end());
     }
     // the same taps interleaved per axis, (sigma1[j], sigma2[j]) pairs, for the fused kernels
+    // (k_dog_z reads the z taps as a symmetric half)
+    for (int j = 0; j < K; ++j)
+        SD_CHECK(k1[2][j] == k1[2][K - 1 - j] && k2[2][j] == k2[2][K - 1 - j], SPIMDECON_ERR_STATE,
+                 "asymmetric z taps");
     for (int a = 0; a < 3; ++a)
         for (int j = 0; j < K; ++j) {
             kall.push_back(k1[a][j]);
@@ -1299,12 +1340,14 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     // (chunk + 2 + KW - 1 source planes must fit k_dog_z's kDzMaxLen plane table)
     const int zc = std::min(kDzMaxLen - 128, std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk)));
     const int ty = dog_env("SPIMDECON_DOG_XY_TY", 48) == 32 ? 32 : 48;
-    const int by = dog_env("SPIMDECON_DOG_Z_BY", 8) == 16 ? 16 : 8;
     const int xcd = dog_env("SPIMDECON_DOG_XCD", 1);   // XCD-contiguous y-fastest boxes of k_dog_z
-    const int pd = dog_env("SPIMDECON_DOG_PD", kDzPD);  // k_dog_z planes loaded ahead (3 for A/B runs)
-    const dim3 gxy(unsigned(ceil_div(d.nx, kDxyTX)), unsigned(ceil_div(d.ny, ty)), unsigned(d.nz));
-    const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, kDzBX - 2))),
-                  unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, by - 2))), unsigned(ceil_div(d.nz, zc)));
+    // k_dog_xy: persistent blocks (3 per CU: 53.6 KB of LDS each, 16 rounds of them), tiles x fastest
+    const int64_t xy_tiles = ceil_div(d.nx, kDxyTX) * ceil_div(d.ny, ty) * d.nz;
+    const dim3 gxy(unsigned(std::min<int64_t>(xy_tiles, int64_t(256) * 3 * dog_env("SPIMDECON_DOG_XY_ROUNDS", 16))));
+    const int bx = dog_env("SPIMDECON_DOG_Z_BX", 64) == 32 ? 32 : 64;   // box 64 x 8 or 32 x 16
+    const int bz_y = bx == 32 ? 16 : 8;
+    const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, bx - 2))),
+                  unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, bz_y - 2))), unsigned(ceil_div(d.nz, zc)));
     bool store_dog = need_dog;
     if (fused) {
         grow(w.g12, size_t(n));
@@ -1339,12 +1382,17 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         const PeakSink pk{min_peak, wmin, wmax, T, w.keys.p, w.vals.p, w.recs.p, w.count.p, cap};
         if (fused) {
             float* dst = store_dog ? dogp : nullptr;
-#define SD_DOGZ(KV)                                                                                          \
-            if (by == 16) hipLaunchKernelGGL((k_dog_z<KV, 16, kDzPD>), gz, dim3(kDzBX * 16), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd); \
-            else if (pd == 3) hipLaunchKernelGGL((k_dog_z<KV, 8, 3>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd); \
-            else hipLaunchKernelGGL((k_dog_z<KV, 8, kDzPD>), gz, dim3(kDzBX * 8), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, pk, xcd);
+            grow(w.sink, 1);
+            SD_HIP(hipMemcpyAsync(w.sink.p, &pk, sizeof(pk), hipMemcpyHostToDevice, s));   // (synchronised below)
+            const bool one = uint64_t(n) * 4u < 0x80000000ull;
+            const int want = wmin | (wmax << 1);
+#define SD_DOGZ2(KV, BYV, BXV)                                                                                \
+            if (one) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, BXV, true>), gz, dim3(512), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd); \
+            else hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, BXV, false>), gz, dim3(512), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd);
+#define SD_DOGZ(KV) if (bx == 32) { SD_DOGZ2(KV, 16, 32) } else { SD_DOGZ2(KV, 8, 64) }
             if (K == 7) { SD_DOGZ(7) } else if (K == 15) { SD_DOGZ(15) } else { SD_DOGZ(31) }
 #undef SD_DOGZ
+#undef SD_DOGZ2
         } else {
             hipLaunchKernelGGL(k_peaks_append, dim3(grid_of(n)), dim3(kBlock), 0, s, dogp, d, pk);
         }

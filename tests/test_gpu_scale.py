@@ -114,6 +114,7 @@ def tiled_views(shape_zyx, V, cid, base=(256, 512, 512), hole=None):
     norm = torch.clamp(sum(prof), min=1.0)
     reps = [-(-nz // base[0]), -(-ny // base[1]), -(-nx // base[2])]
     for v in range(V):
+        print(f"  [tiled views] view {v} of {V} ({nx}x{ny}x{nz})", flush=True)   # (progress: long test)
         img = bimgs[v].repeat(*reps)[:nz, :ny, :nx].contiguous()
         w = (prof[v] / norm).expand(nz, ny, nx).contiguous()
         if hole is not None:

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-3: k_dog_z with symmetric-half taps, sink by pointer, ONE template (SGPR spills)
+export TMPDIR=/tmp
+O=gpurun_out/r3j
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dog.py tests/test_gpu_configs.py::test_c4_dog_768_matches_oracle_on_crops -x -q --timeout 250 --timeout-method thread > $O/dog_tests.log 2>&1 || exit 1
+tools/dog_ab.sh $O/dogab "SPIMDECON_DOG_XCD=1" "SPIMDECON_DOG_XCD=0" "SPIMDECON_DOG_ZCHUNK=256" || exit 2
+tools/pmc_dog.sh $O/dogpmc || exit 3
