@@ -14,7 +14,8 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "libspimdecon.so"
+# SPIMDECON_LIB: an experiment build of the same sources (tools/build_variant.sh) for A/B runs
+LIB_PATH = Path(os.environ.get("SPIMDECON_LIB") or Path(__file__).resolve().parent / "libspimdecon.so")
 
 _i32, _i64, _f32, _f64 = C.c_int32, C.c_int64, C.c_float, C.c_double
 _pf = C.POINTER(C.c_float)

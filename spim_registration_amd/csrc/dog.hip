@@ -434,7 +434,6 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     const int gx = (nx + kDxyTX - 1) / kDxyTX, gy = (ny + TY - 1) / TY;
     const int ntiles = gx * gy * int(d.nz);
     const int t = threadIdx.x;
-    (void)xcd;
     // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
     bool norm = false;
     float mn = 0.0f, diff = 1.0f, rd = 1.0f;
@@ -479,8 +478,15 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     };
     // persistent blocks: the next tile's input values are loaded into registers while
     // this tile is transformed (one tile per block exposed the HBM latency of staging)
+    // xcd: blocks go round-robin to the 8 XCDs (each its own L2); the logical block index
+    // makes XCD k's blocks a contiguous range, so the tiles one XCD holds at a time are x
+    // and y neighbours whose halo lines its L2 serves (else they come from HBM twice)
     float v[NE];
-    int tile = blockIdx.x;
+    int tile = int(blockIdx.x);
+    if (xcd) {
+        const unsigned b = blockIdx.x, k = b & 7u, j = b >> 3, q = gridDim.x >> 3, r = gridDim.x & 7u;
+        tile = int(k * q + min(k, r) + j);
+    }
     if (tile < ntiles) stage_loads(tile, v);
     for (; tile < ntiles; tile += gridDim.x) {
         int x0, y0;
@@ -611,6 +617,9 @@ __device__ __forceinline__ void sink_append(const PeakSink& pk, bool flag, int x
 // LDS and go to the sink 64 at a time (one global atomic per flush instead of one per
 // wave-step with a candidate; its returned value is the only vmcnt(0) in the loop)
 constexpr int kCandBuf = 64;
+#ifndef SPIMDECON_DZ_EXP
+#define SPIMDECON_DZ_EXP 0   // experiment builds only (tools/build_variant.sh)
+#endif
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -679,7 +688,10 @@ __device__ __noinline__ int dz_special_nan(const float* Dr, int by, int bx, int 
 // the scalar offset); else a resource per plane.  want: bit 0 minima, bit 1 maxima.
 // The z taps are symmetric (gaussian_kernel builds them so): taps j and KW - 1 - j are
 // the same value and only R + 1 of them are held in SGPRs.
-template <int KW, int BY, int PD, int BX, bool ONE>
+// SL: the source plane of each load from scalar mirror arithmetic (needs nz > KW / 2: one
+// reflection) and a buffer resource per plane, so the load's address is the column's
+// constant byte offset; else the LDS plane table and a 64-bit address per load.
+template <int KW, int BY, int PD, int BX, bool ONE, bool SL>
 __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
                                                          const float2* __restrict__ kz, float scale, int zc_len,
                                                          float* __restrict__ dog, float minv, int want,
@@ -715,14 +727,26 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     // element offset of the source plane of every window index (mirror-single
     // extension, the tail repeating the last plane): a table read per load instead of
     // scalar index arithmetic per unrolled step (that spilled SGPRs)
-    __shared__ uint32_t zoff[kDzMaxLen];
-    for (int i = t; i < kDzMaxLen; i += BX * BY)
-        zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
+    __shared__ uint32_t zoff[SL ? 1 : kDzMaxLen];
+    if constexpr (!SL)
+        for (int i = t; i < kDzMaxLen; i += BX * BY)
+            zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
     if (t < 4) nanq[t] = -1;
     __syncthreads();
     // unconditional loads (columns outside the volume read column 0): no branch merge,
     // so they stay in flight PD planes ahead
-    auto ld = [&](int i) -> float2 { return g12[zoff[min(i, kDzMaxLen - 1)] + col]; };
+    const uint32_t plane_bytes = pstride * 8u;
+    auto ld = [&](int i) -> float2 {
+        if constexpr (SL) {
+            const int tz = qa - R + min(i, len - 1);
+            const int m = (nz - 1) - abs((nz - 1) - abs(tz));   // mirror-single, one reflection
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float2*>(g12) + size_t(uint32_t(m)) * pstride, 0, int(plane_bytes), 0x00020000);
+            return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(col * 8u), 0, 0));
+        } else {
+            return g12[zoff[min(i, kDzMaxLen - 1)] + col];
+        }
+    };
     // step s: window = source planes s .. s + KW - 1 in slots (s + j) % NW, DoG plane
     // q = qa + s; the step count is padded to whole NW rotations (padded steps test and
     // store nothing), so the unrolled body has no exits
@@ -745,12 +769,16 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
             const int st = sb + ph;
             w[(ph + NW - 1) % NW] = ld(st + NW - 1);
             dg_v2 acc = {0.0f, 0.0f};
+#if SPIMDECON_DZ_EXP == 2   // (experiment build: loads without the convolution)
+            acc = dg_v2{w[ph % NW].x, w[ph % NW].y};
+#else
 #pragma unroll
             for (int j = 0; j < KW; ++j) {   // tap order kept
                 const float2 v = w[(ph + j) % NW];
                 const float2 k = kz[j <= R ? j : KW - 1 - j];
                 acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
             }
+#endif
             const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
             const int q = qa + st;
             {   // the DoG store: a buffer store, dropped (out of range) unless owned
@@ -765,6 +793,10 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd, vo, 0, 0);
                 }
             }
+#if SPIMDECON_DZ_EXP == 1   // (experiment build: the convolution without the peak test)
+            if (dv == 12345.0f) cbuf[0][0].x = q;
+            continue;
+#endif
             const int slot = q & 3;
             Dr[slot][ty][tx] = dv;
             if (__ballot(dv != dv) != 0ull && tx == 0) nanq[slot] = q;
@@ -1341,19 +1373,22 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     const int zc = std::min(kDzMaxLen - 128, std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk)));
     const int ty = dog_env("SPIMDECON_DOG_XY_TY", 48) == 32 ? 32 : 48;
     const int xcd = dog_env("SPIMDECON_DOG_XCD", 1);   // XCD-contiguous y-fastest boxes of k_dog_z
+    const int xcd_xy = dog_env("SPIMDECON_DOG_XY_XCD", 1);   // XCD-contiguous tile ranges of k_dog_xy
     // k_dog_xy: persistent blocks (3 per CU: 53.6 KB of LDS each, 16 rounds of them), tiles x fastest
     const int64_t xy_tiles = ceil_div(d.nx, kDxyTX) * ceil_div(d.ny, ty) * d.nz;
     const dim3 gxy(unsigned(std::min<int64_t>(xy_tiles, int64_t(256) * 3 * dog_env("SPIMDECON_DOG_XY_ROUNDS", 16))));
-    const int bx = dog_env("SPIMDECON_DOG_Z_BX", 64) == 32 ? 32 : 64;   // box 64 x 8 or 32 x 16
-    const int bz_y = bx == 32 ? 16 : 8;
+    // k_dog_z box: 64 x 8 (512 threads) or 64 x 16 (1024); 32 x 16 measured slower (r3i)
+    const int bx = 64, bz_y = dog_env("SPIMDECON_DOG_Z_BY", 8) == 16 ? 16 : 8;
+    // scalar plane indices (one mirror reflection: nz > K / 2; plane bytes in 31 bits)
+    const bool zsl = dog_env("SPIMDECON_DOG_Z_TBL", 0) == 0 && d.nz > K / 2 && d.nx * d.ny * 8 < (int64_t(1) << 31);
     const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, bx - 2))),
                   unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, bz_y - 2))), unsigned(ceil_div(d.nz, zc)));
     bool store_dog = need_dog;
     if (fused) {
         grow(w.g12, size_t(n));
 #define SD_DOGXY(KV)                                                                                        \
-        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd);
+        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy);
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
@@ -1386,13 +1421,15 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
             SD_HIP(hipMemcpyAsync(w.sink.p, &pk, sizeof(pk), hipMemcpyHostToDevice, s));   // (synchronised below)
             const bool one = uint64_t(n) * 4u < 0x80000000ull;
             const int want = wmin | (wmax << 1);
-#define SD_DOGZ2(KV, BYV, BXV)                                                                                \
-            if (one) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, BXV, true>), gz, dim3(512), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd); \
-            else hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, BXV, false>), gz, dim3(512), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd);
-#define SD_DOGZ(KV) if (bx == 32) { SD_DOGZ2(KV, 16, 32) } else { SD_DOGZ2(KV, 8, 64) }
+#define SD_DOGZ4(KV, BYV, ONEV, SLV) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, 64, ONEV, SLV>), gz, dim3(64 * BYV), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd);
+#define SD_DOGZ3(KV, ONEV, SLV) if (bz_y == 16) { SD_DOGZ4(KV, 16, ONEV, SLV) } else { SD_DOGZ4(KV, 8, ONEV, SLV) }
+#define SD_DOGZ2(KV, ONEV) if (zsl) { SD_DOGZ3(KV, ONEV, true) } else { SD_DOGZ3(KV, ONEV, false) }
+#define SD_DOGZ(KV) if (one) { SD_DOGZ2(KV, true) } else { SD_DOGZ2(KV, false) }
             if (K == 7) { SD_DOGZ(7) } else if (K == 15) { SD_DOGZ(15) } else { SD_DOGZ(31) }
 #undef SD_DOGZ
 #undef SD_DOGZ2
+#undef SD_DOGZ3
+#undef SD_DOGZ4
         } else {
             hipLaunchKernelGGL(k_peaks_append, dim3(grid_of(n)), dim3(kBlock), 0, s, dogp, d, pk);
         }
