@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     }
 }
 
-struct PeakOut {
+struct PeakOut {   // (k_dog_z's cand_flush writes it as three int pairs)
     int32_t x, y, z;
     float intensity;
     int32_t is_min, is_max;
@@ -629,6 +629,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // (the sink is read through a pointer: its fields are loaded here, at a flush, instead of
 // holding 10 SGPRs for the whole z loop)
+// (global-address-space stores and atomic: flat ones count in both vmcnt and lgkmcnt,
+// and a flat operation pending at a join made every later load wait in k_dog_z's
+// loop a vmcnt(0) -- the plane prefetch drained three times per unrolled rotation)
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
 __device__ __forceinline__ void cand_flush(const PeakSink* __restrict__ sink, const int4* buf, int n, int nx,
                                            uint32_t pstride) {
     if (n == 0) return;
@@ -636,23 +643,22 @@ __device__ __forceinline__ void cand_flush(const PeakSink* __restrict__ sink, co
     const PeakSink pk = *sink;
     const int lane = int(threadIdx.x & 63);
     unsigned base = 0;
-    if (lane == 0) base = atomicAdd(pk.count, unsigned(n));
+    if (lane == 0)
+        base = __hip_atomic_fetch_add(gbl(pk.count), unsigned(n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = unsigned(__shfl(int(base), 0, 64));
     if (lane < n) {
         const int4 e = buf[lane];
         const unsigned pos = base + unsigned(lane);
         if (pos < pk.cap) {
             const int x = e.x, y = e.y & 0x3fffffff, sp = int(unsigned(e.y) >> 30), z = e.z;
-            pk.keys[pos] = (uint64_t(x % pk.T) << 40) | (uint64_t(z) * pstride + uint64_t(y) * uint32_t(nx) + x);
-            pk.vals[pos] = pos;
-            PeakOut o;
-            o.x = x;
-            o.y = y;
-            o.z = z;
-            o.intensity = __int_as_float(e.w);
-            o.is_min = sp == 1;
-            o.is_max = sp == 2;
-            pk.recs[pos] = o;
+            *gbl(pk.keys + pos) = (uint64_t(x % pk.T) << 40) | (uint64_t(z) * pstride + uint64_t(y) * uint32_t(nx) + x);
+            *gbl(pk.vals + pos) = pos;
+            // the PeakOut record {x, y, z, intensity, is_min, is_max} as three 8-B stores
+            typedef int v2i __attribute__((ext_vector_type(2)));
+            v2i* r = reinterpret_cast<v2i*>(pk.recs + pos);
+            *gbl(r) = v2i{x, y};
+            *gbl(r + 1) = v2i{z, e.w};
+            *gbl(r + 2) = v2i{sp == 1 ? 1 : 0, sp == 2 ? 1 : 0};
         }
     }
     wave_lds_sync();   // the buffer is rewritten after the flush
@@ -737,6 +743,16 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     // so they stay in flight PD planes ahead
     const uint32_t plane_bytes = pstride * 8u;
     auto ld = [&](int i) -> float2 {
+#if SPIMDECON_DZ_EXP == 3   // (experiment build: the access pattern of a brick layout, values wrong)
+        {
+            const int tz = qa - R + min(i, len - 1);
+            const int m = (nz - 1) - abs((nz - 1) - abs(tz));
+            const uint32_t boxl = uint32_t(bb.by) * gridDim.x + bb.bx, ntot = pstride * uint32_t(nz);
+            uint32_t e = (boxl * uint32_t(nz) + uint32_t(m)) * uint32_t(BX * BY) + uint32_t(t);
+            e = e >= ntot ? e - ntot : e;
+            return g12[e];
+        }
+#endif
         if constexpr (SL) {
             const int tz = qa - R + min(i, len - 1);
             const int m = (nz - 1) - abs((nz - 1) - abs(tz));   // mirror-single, one reflection
@@ -1241,7 +1257,18 @@ struct DogWork {
     DBuf<unsigned char> flags, sel_tmp;
     DBuf<int> nsel;
     DBuf<PeakSink> sink;                   // k_dog_z's sink, read at its flushes
+    // the calls' stream, created once (a stream per call cost ~1 ms of host time per
+    // 768^3 call: r3l trace, 1.17 ms before the first copy)
+    hipStream_t stream = nullptr;
+    hipStream_t get_stream() {
+        if (!stream) SD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        return stream;
+    }
     void release() {
+        if (stream) {
+            (void)hipStreamDestroy(stream);
+            stream = nullptr;
+        }
         for (DBuf<float>* b : {&in, &dog, &taps, &mm, &tmp_a, &tmp_b, &tmp_c, &tmp_d}) b->release();
         g12.release();
         keys.release(); keys_sorted.release(); vals.release(); vals_sorted.release();
@@ -1459,10 +1486,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     if (dog_out && !dog_dev) SD_HIP(hipMemcpyAsync(dog_out, dogp, n * 4, hipMemcpyDefault, s));
 }
 
-struct StreamHolder {
+struct StreamHolder {   // the workspace's stream (held under its mutex)
     hipStream_t s = nullptr;
-    StreamHolder() { SD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
-    ~StreamHolder() { (void)hipStreamDestroy(s); }
+    explicit StreamHolder(DogWork& w) : s(w.get_stream()) {}
 };
 
 // DifferenceOfGaussianNewPeakFinder.getSimplePeaks level: candidates with
@@ -1474,7 +1500,7 @@ void dog_compute(const float* img, const int64_t* dims, const spim_dog_params* p
     DeviceGuard guard(p->device);
     DogWork& w = dog_work(p->device);
     std::lock_guard<std::mutex> lk(w.mu);
-    StreamHolder sh;
+    StreamHolder sh(w);
     DogRun r;
     dog_run(img, dims, p, dog_out, dog_out != nullptr, sh.s, w, r);
     *npeaks = r.np;
@@ -1526,7 +1552,7 @@ void dog_interest_points(const float* img, const int64_t* dims, const spim_dog_p
     DeviceGuard guard(p->device);
     DogWork& w = dog_work(p->device);
     std::lock_guard<std::mutex> lk(w.mu);
-    StreamHolder sh;
+    StreamHolder sh(w);
     DogRun r;
     dog_run(img, dims, p, dog_out, p->localization == 1 || dog_out != nullptr, sh.s, w, r);
     const int64_t np = r.np;
