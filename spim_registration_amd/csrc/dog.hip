@@ -356,7 +356,10 @@ constexpr int kDxyTX = 64;   // xy tile: outputs along x (TY along y: template)
 constexpr int kDxySeg = 8;   // x outputs per thread in the x phase (register window)
 constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave per row, the
                              // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
-constexpr int kDzPD = 8;     // planes loaded ahead of use: 3 left the HBM latency exposed
+#ifndef SPIMDECON_DZ_PD
+#define SPIMDECON_DZ_PD 8
+#endif
+constexpr int kDzPD = SPIMDECON_DZ_PD;   // planes loaded ahead of use: 3 left the HBM latency exposed
                              // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
 constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
@@ -620,6 +623,22 @@ constexpr int kCandBuf = 64;
 #ifndef SPIMDECON_DZ_EXP
 #define SPIMDECON_DZ_EXP 0   // experiment builds only (tools/build_variant.sh)
 #endif
+// (experiment builds: parts of k_dog_z removed to time the rest; values wrong)
+#define DZ_NOTEST (SPIMDECON_DZ_EXP == 1 || (SPIMDECON_DZ_EXP >= 4 && SPIMDECON_DZ_EXP <= 6))
+#define DZ_NOCONV (SPIMDECON_DZ_EXP == 2 || SPIMDECON_DZ_EXP == 6)
+#define DZ_NOSTORE ((SPIMDECON_DZ_EXP >= 4 && SPIMDECON_DZ_EXP <= 6) || SPIMDECON_DZ_EXP == 8 || SPIMDECON_DZ_EXP == 10)
+#define DZ_NOLOAD (SPIMDECON_DZ_EXP == 5)
+#ifndef DZ_PIPE
+#define DZ_PIPE 1
+#endif
+#if SPIMDECON_DZ_EXP == 9          // every plane's stores to plane 0 (L2-resident writes)
+#define DZ_STORE_SOFF(x) 0
+#else
+#define DZ_STORE_SOFF(x) (x)
+#endif
+#ifndef DZ_STORE_AUX
+#define DZ_STORE_AUX 0             // (cache-policy bits of the DoG store; experiments set nt)
+#endif
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -737,7 +756,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     if constexpr (!SL)
         for (int i = t; i < kDzMaxLen; i += BX * BY)
             zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
-    if (t < 4) nanq[t] = -1;
+    if (t < 4) nanq[t] = INT_MIN;   // (no plane)
     __syncthreads();
     // unconditional loads (columns outside the volume read column 0): no branch merge,
     // so they stay in flight PD planes ahead
@@ -769,7 +788,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     float2 w[NW];
 #pragma unroll
     for (int p = 0; p < NW - 1; ++p) w[p] = ld(p);
-    const int nsteps = (qb - qa + NW - 1) / NW * NW;
+    const int nsteps = (qb - qa + DZ_PIPE + NW - 1) / NW * NW;   // (one more step when pipelined)
     float mnA = 0.f, mxA = 0.f, mnB = 0.f, mxB = 0.f, mnC = 0.f, mxC = 0.f, dB = 0.f, dC = 0.f;
     int nanhist = 0;   // bit k: the block's DoG plane q - k holds a NaN
     // DoG stores: one buffer resource over the whole image with the plane in the scalar
@@ -779,13 +798,19 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                                                                           0x00020000);
     const uint32_t dog_bytes = dog ? pstride * 4u : 0u;
     const bool want_min = (want & 1) != 0, want_max = (want & 2) != 0;
+    float exp_sink = 0.0f;   // (experiment builds)
+    float dprev = 0.0f;      // (DZ_PIPE: the DoG value of the previous plane)
     for (int sb = 0; sb < nsteps; sb += NW) {
 #pragma unroll
         for (int ph = 0; ph < NW; ++ph) {
             const int st = sb + ph;
+#if DZ_NOLOAD
+            w[(ph + NW - 1) % NW] = make_float2(w[ph % NW].y, w[(ph + 1) % NW].x);
+#else
             w[(ph + NW - 1) % NW] = ld(st + NW - 1);
+#endif
             dg_v2 acc = {0.0f, 0.0f};
-#if SPIMDECON_DZ_EXP == 2   // (experiment build: loads without the convolution)
+#if DZ_NOCONV   // (experiment build: loads without the convolution)
             acc = dg_v2{w[ph % NW].x, w[ph % NW].y};
 #else
 #pragma unroll
@@ -797,39 +822,70 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
 #endif
             const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
             const int q = qa + st;
-            {   // the DoG store: a buffer store, dropped (out of range) unless owned
+            if (!DZ_NOSTORE) {   // the DoG store: a buffer store, dropped (out of range) unless owned
                 const bool st_ok = own && q >= z0 && q < z1;
+#if SPIMDECON_DZ_EXP == 7   // (experiment build: 64-aligned full-line DoG row stores, values misplaced)
+                const bool st7 = valid && (ty >= (bb.by == 0 ? 0 : 1)) && (lasty || ty < BY - 1) && q >= z0 && q < z1;
+                const int vo = int(st7 && bb.bx * 64 + tx < nx ? (uint32_t(y) * uint32_t(nx) + uint32_t(bb.bx * 64 + tx)) * 4u
+                                                                : 0x80000000u);
+#elif SPIMDECON_DZ_EXP == 11   // every store out of range (issued, no traffic)
+                const int vo = int(st_ok && q < 0 ? col * 4u : 0x80000000u);
+#else
                 const int vo = int(st_ok ? col * 4u : 0x80000000u);
+#endif
                 if constexpr (ONE) {
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
-                                                          int(uint32_t(min(q, nz - 1)) * pstride * 4u), 0);
+                                                          DZ_STORE_SOFF(int(uint32_t(min(q, nz - 1)) * pstride * 4u)), DZ_STORE_AUX);
                 } else {
                     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                         dog + (dog ? size_t(min(q, nz - 1)) * pstride : 0), 0, int(dog_bytes), 0x00020000);
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd, vo, 0, 0);
                 }
             }
-#if SPIMDECON_DZ_EXP == 1   // (experiment build: the convolution without the peak test)
-            if (dv == 12345.0f) cbuf[0][0].x = q;
+#if DZ_NOTEST   // (experiment build: without the peak test)
+            exp_sink += dv;
             continue;
 #endif
+#if DZ_PIPE
+            // software-pipelined by one plane: plane q - 1's ring row went in at the end of
+            // the previous step, so this step's loads and convolution lie between that
+            // write and the barrier (a wave behind the others catches up there instead of
+            // the whole block idling at a barrier right behind its own LDS write)
+            const int qt = q - 1;                // the plane tested into the box history
+            const float dcur = dprev;
+            const int slot = qt & 3;
+#else
+            const int qt = q;
+            const float dcur = dv;
             const int slot = q & 3;
             Dr[slot][ty][tx] = dv;
             if (__ballot(dv != dv) != 0ull && tx == 0) nanq[slot] = q;
+#endif
             lds_barrier();
-            nanhist = ((nanhist << 1) | (nanq[slot] == q ? 1 : 0)) & 7;
+#if SPIMDECON_DZ_EXP == 8   // (experiment build: one wave stores the plane's box from LDS, 16-B pieces)
+            if (wv == (q & (BX * BY / 64 - 1)) && q >= z0 && q < z1) {
+                for (int k = lane; k < BY * BX / 4; k += 64) {
+                    const int r = k / (BX / 4), c4 = (k % (BX / 4)) * 4;
+                    const float4 v4 = *reinterpret_cast<const float4*>(&Dr[slot][r][c4]);
+                    const uint32_t off = ((uint32_t(min(Y0 + r, ny - 1)) * uint32_t(nx) + uint32_t(X0 + c4)) & ~3u) * 4u;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v4), rall, int(off),
+                                                           int(uint32_t(q) * pstride * 4u), 0);
+                }
+            }
+#endif
+            nanhist = ((nanhist << 1) | (nanq[slot] == qt ? 1 : 0)) & 7;
             mnA = mnB; mxA = mxB; mnB = mnC; mxB = mxC;
             dB = dC;
-            dC = dv;
+            dC = dcur;
             {   // 3x3 box of this plane (the centre included), every lane
                 const float (*P)[BX] = Dr[slot];
                 const float a0 = P[yu][xl], a1 = P[yu][tx], a2 = P[yu][xr];
                 const float b0 = P[ty][xl], b2 = P[ty][xr];
                 const float c0 = P[yd][xl], c1 = P[yd][tx], c2 = P[yd][xr];
-                mnC = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, fminf(c2, dv))));
-                mxC = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, fmaxf(c2, dv))));
+                mnC = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, fminf(c2, dcur))));
+                mxC = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, fmaxf(c2, dcur))));
             }
-            const int zc = q - 1;   // centre plane of the test
+            const int zc = qt - 1;   // centre plane of the test
             if (zc >= tlo && zc < thi) {
                 const float c = dB;
                 const bool cand = inner && !(fabsf(c) < minv);
@@ -856,8 +912,14 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                     ccount += nb;
                 }
             }
+#if DZ_PIPE
+            Dr[q & 3][ty][tx] = dv;
+            if (__ballot(dv != dv) != 0ull && tx == 0) nanq[q & 3] = q;
+            dprev = dv;
+#endif
         }
     }
+    if (exp_sink == 12345.0f) atomicAdd(sink->count, 1u);   // (a global side effect keeps it live)
     cand_flush(sink, cbuf[wv], ccount, nx, pstride);
 }
 
