@@ -356,10 +356,9 @@ constexpr int kDxyTX = 64;   // xy tile: outputs along x (TY along y: template)
 constexpr int kDxySeg = 8;   // x outputs per thread in the x phase (register window)
 constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave per row, the
                              // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
-#ifndef SPIMDECON_DZ_PD
-#define SPIMDECON_DZ_PD 8
-#endif
-constexpr int kDzPD = SPIMDECON_DZ_PD;   // planes loaded ahead of use: 3 left the HBM latency exposed
+// planes loaded ahead of use (3 left the HBM latency exposed; 12 or 16 no better, 16
+// costs a wave per SIMD); KW + kDzPD must be a multiple of 4 (the ring slots)
+constexpr int kDzPD = 9;
                              // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
 constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
@@ -620,26 +619,6 @@ __device__ __forceinline__ void sink_append(const PeakSink& pk, bool flag, int x
 // LDS and go to the sink 64 at a time (one global atomic per flush instead of one per
 // wave-step with a candidate; its returned value is the only vmcnt(0) in the loop)
 constexpr int kCandBuf = 64;
-#ifndef SPIMDECON_DZ_EXP
-#define SPIMDECON_DZ_EXP 0   // experiment builds only (tools/build_variant.sh)
-#endif
-// (experiment builds: parts of k_dog_z removed to time the rest; values wrong)
-#define DZ_NOTEST (SPIMDECON_DZ_EXP == 1 || (SPIMDECON_DZ_EXP >= 4 && SPIMDECON_DZ_EXP <= 6))
-#define DZ_NOCONV (SPIMDECON_DZ_EXP == 2 || SPIMDECON_DZ_EXP == 6)
-#define DZ_NOSTORE ((SPIMDECON_DZ_EXP >= 4 && SPIMDECON_DZ_EXP <= 6) || SPIMDECON_DZ_EXP == 8 || SPIMDECON_DZ_EXP == 10)
-#define DZ_NOLOAD (SPIMDECON_DZ_EXP == 5)
-#ifndef DZ_PIPE
-#define DZ_PIPE 1
-#endif
-#if SPIMDECON_DZ_EXP == 9          // every plane's stores to plane 0 (L2-resident writes)
-#define DZ_STORE_SOFF(x) 0
-#else
-#define DZ_STORE_SOFF(x) (x)
-#endif
-#ifndef DZ_STORE_AUX
-#define DZ_STORE_AUX 0             // (cache-policy bits of the DoG store; experiments set nt)
-#endif
-
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -689,26 +668,51 @@ __device__ __forceinline__ void cand_flush(const PeakSink* __restrict__ sink, co
 // 26-neighbour test is min / max of the 3x3x3 box (the box includes the centre, so
 // "all neighbours >= c" <=> box min >= c); a plane holding a NaN takes the
 // reference's comparison loop instead (NaN compares false).
-// InteractiveIntegral.isSpecialPoint (:443-468) over the 4-plane ring Dr[4][by][BX]
-// (centre plane zc, row ty, column tx): 2 = every neighbour >= c ("MAX"), 1 = every
-// neighbour <= c, 0 = neither.  Only for boxes holding a NaN (compares false), out of
-// line: the min / max test covers every other box.
-__device__ __noinline__ int dz_special_nan(const float* Dr, int by, int bx, int zc, int ty, int tx, float c) {
+//
+// The ring: slot = (plane - qa) & 3, a compile-time constant of the unrolled step (NW is
+// a multiple of 4), rows padded by one above and below and one element before and after,
+// so the 3x3 neighbourhood is ONE per-thread address plus eight immediate offsets (edge
+// lanes read a neighbouring row's element or a pad -- they are never tested).  The
+// step's VALU work is the convolution's 2 KW packed ops plus ~20 for the test: the test
+// had cost as much VALU as the convolution (r3t cost split).
+template <int BY, int BX>
+struct DzRing {
+    static constexpr int kRow = BX, kSlot = (BY + 2) * BX, kSize = 4 * kSlot + 2;
+    // element (slot, row r in [-1, BY], column c in [-1, BX])
+    static __device__ __forceinline__ int at(int slot, int r, int c) { return 1 + slot * kSlot + (r + 1) * kRow + c; }
+};
+
+// InteractiveIntegral.isSpecialPoint (:443-468) over the ring (centre plane slot sc,
+// row ty, column tx): 2 = every neighbour >= c ("MAX"), 1 = every neighbour <= c, 0 =
+// neither.  Only for boxes holding a NaN (compares false), out of line.
+template <int BY, int BX>
+__device__ __noinline__ int dz_special_nan(const float* Dr, int sc, int ty, int tx, float c) {
     bool ge = true, le = true;
     for (int dz = -1; dz <= 1; ++dz)
         for (int dy = -1; dy <= 1; ++dy)
             for (int dx = -1; dx <= 1; ++dx) {
                 if (dz == 0 && dy == 0 && dx == 0) continue;
-                const float v = Dr[(((zc + dz) & 3) * by + ty + dy) * bx + tx + dx];
+                const float v = Dr[DzRing<BY, BX>::at((sc + dz) & 3, ty + dy, tx + dx)];
                 ge &= v >= c;
                 le &= v <= c;
             }
     return ge ? 2 : (le ? 1 : 0);
 }
 
-// BX x BY columns per block (BX * BY = 512 threads): 64 x 8 = one wave per row, or 32 x
-// 16 = two rows per wave -- fewer recomputed halo columns (32 x 16 tests 30 x 14 of 512
-// columns, 64 x 8 only 62 x 6)
+// min / max of three, one instruction (NaN-free inputs: planes holding a NaN take
+// dz_special_nan; minnum / maxnum would add canonicalising maxes of the LDS values)
+__device__ __forceinline__ float dz_min3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float dz_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// BX x BY columns per block (64 x 8: one wave per row; 62 x 6 of them tested).
 // ONE: the DoG image is below 2 GiB, one buffer resource covers it (the plane goes in
 // the scalar offset); else a resource per plane.  want: bit 0 minima, bit 1 maxima.
 // The z taps are symmetric (gaussian_kernel builds them so): taps j and KW - 1 - j are
@@ -723,7 +727,9 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                                                          const PeakSink* __restrict__ sink, int xcd) {
     constexpr int R = KW / 2;
     constexpr int NW = KW + PD;
-    __shared__ float Dr[4][BY][BX];
+    static_assert(NW % 4 == 0, "ring slots are compile-time: the unrolled rotation is whole ring turns");
+    using Ring = DzRing<BY, BX>;
+    __shared__ float Dr[Ring::kSize];
     __shared__ int nanq[4];
     __shared__ int4 cbuf[BX * BY / 64][kCandBuf];   // one candidate buffer per wave
     int ccount = 0;                       // wave-uniform fill of this wave's buffer
@@ -746,12 +752,8 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                      ty >= (bb.by == 0 ? 0 : 1) && (lasty || ty < BY - 1);
     const bool inner = valid && tx >= 1 && tx < BX - 1 && ty >= 1 && ty < BY - 1 && x <= nx - 2 &&
                        y <= ny - 2;
-    // neighbour indices clamped to the box (edge lanes are never `inner`: no branch)
-    const int xl = tx > 0 ? tx - 1 : tx, xr = tx < BX - 1 ? tx + 1 : tx;
-    const int yu = ty > 0 ? ty - 1 : ty, yd = ty < BY - 1 ? ty + 1 : ty;
     // element offset of the source plane of every window index (mirror-single
-    // extension, the tail repeating the last plane): a table read per load instead of
-    // scalar index arithmetic per unrolled step (that spilled SGPRs)
+    // extension, the tail repeating the last plane), for volumes the scalar path cannot take
     __shared__ uint32_t zoff[SL ? 1 : kDzMaxLen];
     if constexpr (!SL)
         for (int i = t; i < kDzMaxLen; i += BX * BY)
@@ -762,16 +764,6 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     // so they stay in flight PD planes ahead
     const uint32_t plane_bytes = pstride * 8u;
     auto ld = [&](int i) -> float2 {
-#if SPIMDECON_DZ_EXP == 3   // (experiment build: the access pattern of a brick layout, values wrong)
-        {
-            const int tz = qa - R + min(i, len - 1);
-            const int m = (nz - 1) - abs((nz - 1) - abs(tz));
-            const uint32_t boxl = uint32_t(bb.by) * gridDim.x + bb.bx, ntot = pstride * uint32_t(nz);
-            uint32_t e = (boxl * uint32_t(nz) + uint32_t(m)) * uint32_t(BX * BY) + uint32_t(t);
-            e = e >= ntot ? e - ntot : e;
-            return g12[e];
-        }
-#endif
         if constexpr (SL) {
             const int tz = qa - R + min(i, len - 1);
             const int m = (nz - 1) - abs((nz - 1) - abs(tz));   // mirror-single, one reflection
@@ -788,7 +780,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     float2 w[NW];
 #pragma unroll
     for (int p = 0; p < NW - 1; ++p) w[p] = ld(p);
-    const int nsteps = (qb - qa + DZ_PIPE + NW - 1) / NW * NW;   // (one more step when pipelined)
+    const int nsteps = (qb - qa + NW - 1) / NW * NW;
     float mnA = 0.f, mxA = 0.f, mnB = 0.f, mxB = 0.f, mnC = 0.f, mxC = 0.f, dB = 0.f, dC = 0.f;
     int nanhist = 0;   // bit k: the block's DoG plane q - k holds a NaN
     // DoG stores: one buffer resource over the whole image with the plane in the scalar
@@ -798,107 +790,74 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                                                                           0x00020000);
     const uint32_t dog_bytes = dog ? pstride * 4u : 0u;
     const bool want_min = (want & 1) != 0, want_max = (want & 2) != 0;
-    float exp_sink = 0.0f;   // (experiment builds)
-    float dprev = 0.0f;      // (DZ_PIPE: the DoG value of the previous plane)
+    float* const rbase = Dr + Ring::at(0, ty - 1, tx - 1);   // this thread's neighbourhood corner
     for (int sb = 0; sb < nsteps; sb += NW) {
 #pragma unroll
         for (int ph = 0; ph < NW; ++ph) {
             const int st = sb + ph;
-#if DZ_NOLOAD
-            w[(ph + NW - 1) % NW] = make_float2(w[ph % NW].y, w[(ph + 1) % NW].x);
-#else
             w[(ph + NW - 1) % NW] = ld(st + NW - 1);
-#endif
             dg_v2 acc = {0.0f, 0.0f};
-#if DZ_NOCONV   // (experiment build: loads without the convolution)
-            acc = dg_v2{w[ph % NW].x, w[ph % NW].y};
-#else
 #pragma unroll
             for (int j = 0; j < KW; ++j) {   // tap order kept
                 const float2 v = w[(ph + j) % NW];
                 const float2 k = kz[j <= R ? j : KW - 1 - j];
                 acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
             }
-#endif
             const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
             const int q = qa + st;
-            if (!DZ_NOSTORE) {   // the DoG store: a buffer store, dropped (out of range) unless owned
+            {   // the DoG store: a buffer store, dropped (out of range) unless owned
                 const bool st_ok = own && q >= z0 && q < z1;
-#if SPIMDECON_DZ_EXP == 7   // (experiment build: 64-aligned full-line DoG row stores, values misplaced)
-                const bool st7 = valid && (ty >= (bb.by == 0 ? 0 : 1)) && (lasty || ty < BY - 1) && q >= z0 && q < z1;
-                const int vo = int(st7 && bb.bx * 64 + tx < nx ? (uint32_t(y) * uint32_t(nx) + uint32_t(bb.bx * 64 + tx)) * 4u
-                                                                : 0x80000000u);
-#elif SPIMDECON_DZ_EXP == 11   // every store out of range (issued, no traffic)
-                const int vo = int(st_ok && q < 0 ? col * 4u : 0x80000000u);
-#else
                 const int vo = int(st_ok ? col * 4u : 0x80000000u);
-#endif
                 if constexpr (ONE) {
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
-                                                          DZ_STORE_SOFF(int(uint32_t(min(q, nz - 1)) * pstride * 4u)), DZ_STORE_AUX);
+                                                          int(uint32_t(min(q, nz - 1)) * pstride * 4u), 0);
                 } else {
                     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
                         dog + (dog ? size_t(min(q, nz - 1)) * pstride : 0), 0, int(dog_bytes), 0x00020000);
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd, vo, 0, 0);
                 }
             }
-#if DZ_NOTEST   // (experiment build: without the peak test)
-            exp_sink += dv;
-            continue;
-#endif
-#if DZ_PIPE
-            // software-pipelined by one plane: plane q - 1's ring row went in at the end of
-            // the previous step, so this step's loads and convolution lie between that
-            // write and the barrier (a wave behind the others catches up there instead of
-            // the whole block idling at a barrier right behind its own LDS write)
-            const int qt = q - 1;                // the plane tested into the box history
-            const float dcur = dprev;
-            const int slot = qt & 3;
-#else
-            const int qt = q;
-            const float dcur = dv;
-            const int slot = q & 3;
-            Dr[slot][ty][tx] = dv;
+            const int slot = ph & 3;   // == (q - qa) & 3 (sb is a multiple of NW, so of 4): a constant once unrolled
+            float* const P = rbase + slot * Ring::kSlot;
+            P[Ring::kRow + 1] = dv;        // (row ty, column tx)
             if (__ballot(dv != dv) != 0ull && tx == 0) nanq[slot] = q;
-#endif
+#ifdef SPIMDECON_DZ_NOBARRIER   // (experiment build: the cost of the per-plane barrier; wrong results)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
             lds_barrier();
-#if SPIMDECON_DZ_EXP == 8   // (experiment build: one wave stores the plane's box from LDS, 16-B pieces)
-            if (wv == (q & (BX * BY / 64 - 1)) && q >= z0 && q < z1) {
-                for (int k = lane; k < BY * BX / 4; k += 64) {
-                    const int r = k / (BX / 4), c4 = (k % (BX / 4)) * 4;
-                    const float4 v4 = *reinterpret_cast<const float4*>(&Dr[slot][r][c4]);
-                    const uint32_t off = ((uint32_t(min(Y0 + r, ny - 1)) * uint32_t(nx) + uint32_t(X0 + c4)) & ~3u) * 4u;
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v4), rall, int(off),
-                                                           int(uint32_t(q) * pstride * 4u), 0);
-                }
-            }
 #endif
-            nanhist = ((nanhist << 1) | (nanq[slot] == qt ? 1 : 0)) & 7;
+            const int nq = __builtin_amdgcn_readfirstlane(nanq[slot]);
+            nanhist = ((nanhist << 1) | (nq == q ? 1 : 0)) & 7;
             mnA = mnB; mxA = mxB; mnB = mnC; mxB = mxC;
             dB = dC;
-            dC = dcur;
+            dC = dv;
             {   // 3x3 box of this plane (the centre included), every lane
-                const float (*P)[BX] = Dr[slot];
-                const float a0 = P[yu][xl], a1 = P[yu][tx], a2 = P[yu][xr];
-                const float b0 = P[ty][xl], b2 = P[ty][xr];
-                const float c0 = P[yd][xl], c1 = P[yd][tx], c2 = P[yd][xr];
-                mnC = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, fminf(c2, dcur))));
-                mxC = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, fmaxf(c2, dcur))));
+                const float a0 = P[0], a1 = P[1], a2 = P[2];
+                const float b0 = P[Ring::kRow], b2 = P[Ring::kRow + 2];
+                const float c0 = P[2 * Ring::kRow], c1 = P[2 * Ring::kRow + 1], c2 = P[2 * Ring::kRow + 2];
+                mnC = dz_min3(dz_min3(a0, a1, a2), dz_min3(b0, b2, c0), dz_min3(c1, c2, dv));
+                mxC = dz_max3(dz_max3(a0, a1, a2), dz_max3(b0, b2, c0), dz_max3(c1, c2, dv));
             }
-            const int zc = qt - 1;   // centre plane of the test
+            const int zc = q - 1;   // centre plane of the test
             if (zc >= tlo && zc < thi) {
                 const float c = dB;
                 const bool cand = inner && !(fabsf(c) < minv);
-                int sp = 0;
+                // "this mixup is intended" (InteractiveIntegral.isSpecialPoint): every
+                // neighbour >= c is a MAX (sp 2), every neighbour <= c a MIN (sp 1); lane
+                // masks, no per-lane branches
+                bool is_max, is_min;
                 if (nanhist == 0) {
-                    const bool ge = fminf(fminf(mnA, mnB), mnC) >= c;
-                    const bool le = fmaxf(fmaxf(mxA, mxB), mxC) <= c;
-                    // "this mixup is intended" (InteractiveIntegral.isSpecialPoint)
-                    sp = cand ? (ge ? 2 : (le ? 1 : 0)) : 0;
-                } else if (cand) {   // a NaN in the box: the reference's comparison loop
-                    sp = dz_special_nan(&Dr[0][0][0], BY, BX, zc, ty, tx, c);
+                    const bool ge = dz_min3(mnA, mnB, mnC) >= c;
+                    const bool le = dz_max3(mxA, mxB, mxC) <= c;
+                    is_max = cand && ge;
+                    is_min = cand && !ge && le;
+                } else {   // a NaN in the box: the reference's comparison loop
+                    const int spn = cand ? dz_special_nan<BY, BX>(Dr, (slot + 3) & 3, ty, tx, c) : 0;
+                    is_max = spn == 2;
+                    is_min = spn == 1;
                 }
-                const bool flag = (sp == 2 && want_max) || (sp == 1 && want_min);
+                const int sp = is_max ? 2 : 1;
+                const bool flag = (is_max && want_max) || (is_min && want_min);
                 const unsigned long long bal = __ballot(flag);
                 if (bal != 0ull) {
                     const int nb = __popcll(bal);
@@ -912,14 +871,8 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                     ccount += nb;
                 }
             }
-#if DZ_PIPE
-            Dr[q & 3][ty][tx] = dv;
-            if (__ballot(dv != dv) != 0ull && tx == 0) nanq[q & 3] = q;
-            dprev = dv;
-#endif
         }
     }
-    if (exp_sink == 12345.0f) atomicAdd(sink->count, 1u);   // (a global side effect keeps it live)
     cand_flush(sink, cbuf[wv], ccount, nx, pstride);
 }
 
