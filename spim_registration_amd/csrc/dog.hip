@@ -358,7 +358,10 @@ constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave pe
                              // outer ring is the peak test's halo (62 x (BY - 2) tested columns)
 // planes loaded ahead of use (3 left the HBM latency exposed; 12 or 16 no better, 16
 // costs a wave per SIMD); KW + kDzPD must be a multiple of 4 (the ring slots)
-constexpr int kDzPD = 9;
+#ifndef SPIMDECON_DZ_PD
+#define SPIMDECON_DZ_PD 9
+#endif
+constexpr int kDzPD = SPIMDECON_DZ_PD;
                              // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
 constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
@@ -821,11 +824,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
             float* const P = rbase + slot * Ring::kSlot;
             P[Ring::kRow + 1] = dv;        // (row ty, column tx)
             if (__ballot(dv != dv) != 0ull && tx == 0) nanq[slot] = q;
-#ifdef SPIMDECON_DZ_NOBARRIER   // (experiment build: the cost of the per-plane barrier; wrong results)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
             lds_barrier();
-#endif
             const int nq = __builtin_amdgcn_readfirstlane(nanq[slot]);
             nanhist = ((nanhist << 1) | (nq == q ? 1 : 0)) & 7;
             mnA = mnB; mxA = mxB; mnB = mnC; mxB = mxC;
