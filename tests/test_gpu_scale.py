@@ -182,7 +182,10 @@ def test_c5_decomposition_matches_oracle_256x256x128(gpu):
         st = s.run(2, 0.006)
         s.apply_mask()
         assert s.num_slabs() == 8 and s.slab_extent(0) == (256, 128, 32)
-        assert_fast(s)
+        # x = 256 + 24 = 280 is not a two-factor tile length (C5's 2100 is: the two tests
+        # above assert xpass 2 at the real geometry); the z pass is the direct one
+        xm, zm = engine_modes(s)
+        assert set(xm) <= {1, 2} and set(zm) <= {2, 3}, (xm, zm)
         psi = s.get_psi()
     hi = [i.astype(np.float16).astype(np.float32) for i in imgs]
     hw = [w.astype(np.float16).astype(np.float32) for w in ws]
