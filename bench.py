@@ -308,7 +308,9 @@ def main(argv=None):
         ny_g = ny
         if strong:   # the global volume is fixed; split along the longer of y and z
             nz_g = nz
-            if ny > nz and N > 1:    # (1024x1024x512: 128 + 24 halo rows per GPU, not 64 + 24 planes)
+            # (1024x1024x512: 128 + 24 halo rows per GPU, not 64 + 24 planes; local slabs
+            # emulate the same decomposition on one GPU)
+            if ny > nz and (N > 1 or args.local_slabs > 1):
                 axis = "y"
             if mode == "ranks":
                 o0, o1 = slab_range(ny_g if axis == "y" else nz_g, world, rank)
