@@ -747,6 +747,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     const int qa = max(z0 - 1, 0), qb = min(z1 + 1, nz);   // DoG planes computed
     const int len = qb - qa + KW - 1;                       // source planes loaded
     const int tlo = max(z0, 1), thi = min(z1, nz - 1);      // centre planes tested
+    const uint32_t ntest = uint32_t(max(thi - tlo, 0));
     const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
     const uint32_t col = valid ? uint32_t(y) * uint32_t(nx) + uint32_t(x) : 0u;
     // DoG store ownership: the tile's tested columns, plus the volume's outer ring
@@ -809,7 +810,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
             const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
             const int q = qa + st;
             {   // the DoG store: a buffer store, dropped (out of range) unless owned
-                const bool st_ok = own && q >= z0 && q < z1;
+                const bool st_ok = own && uint32_t(q - z0) < uint32_t(z1 - z0);
                 const int vo = int(st_ok ? col * 4u : 0x80000000u);
                 if constexpr (ONE) {
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
@@ -838,19 +839,19 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                 mxC = dz_max3(dz_max3(a0, a1, a2), dz_max3(b0, b2, c0), dz_max3(c1, c2, dv));
             }
             const int zc = q - 1;   // centre plane of the test
-            if (zc >= tlo && zc < thi) {
+            if (uint32_t(zc - tlo) < ntest) {   // zc in [tlo, thi)
                 const float c = dB;
                 const bool cand = inner && !(fabsf(c) < minv);
                 // "this mixup is intended" (InteractiveIntegral.isSpecialPoint): every
                 // neighbour >= c is a MAX (sp 2), every neighbour <= c a MIN (sp 1); lane
                 // masks, no per-lane branches
-                bool is_max, is_min;
-                if (nanhist == 0) {
-                    const bool ge = dz_min3(mnA, mnB, mnC) >= c;
-                    const bool le = dz_max3(mxA, mxB, mxC) <= c;
-                    is_max = cand && ge;
-                    is_min = cand && !ge && le;
-                } else {   // a NaN in the box: the reference's comparison loop
+                // (the min / max path for every lane, then -- a uniform branch, rare -- the
+                // comparison loop when a plane of the box held a NaN: no exec-mask merges)
+                const bool ge = dz_min3(mnA, mnB, mnC) >= c;
+                const bool le = dz_max3(mxA, mxB, mxC) <= c;
+                bool is_max = cand && ge;
+                bool is_min = cand && !ge && le;
+                if (nanhist != 0) {   // a NaN in the box: the reference's comparison loop
                     const int spn = cand ? dz_special_nan<BY, BX>(Dr, (slot + 3) & 3, ty, tx, c) : 0;
                     is_max = spn == 2;
                     is_min = spn == 1;
