@@ -364,7 +364,9 @@ constexpr int kDzBX = 64;    // z kernel: a box of 64 x BY columns = one wave pe
 constexpr int kDzPD = SPIMDECON_DZ_PD;
                              // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
-constexpr int kDzMaxLen = 512;   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
+constexpr int kDzMaxLen = 512;
+constexpr int kDpkY = 4;    // k_dog_peaks: rows per lane
+constexpr int kDpkPD = 2;   // k_dog_peaks: planes loaded ahead   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
 
 __device__ __forceinline__ int mirror32(int i, int n) {
     bool o;
@@ -723,13 +725,17 @@ __device__ __forceinline__ float dz_max3(float a, float b, float c) {
 // SL: the source plane of each load from scalar mirror arithmetic (needs nz > KW / 2: one
 // reflection) and a buffer resource per plane, so the load's address is the column's
 // constant byte offset; else the LDS plane table and a 64-bit address per load.
-template <int KW, int BY, int PD, int BX, bool ONE, bool SL>
+// FROMDOG: the split z stage's test pass -- the DoG planes are read from the image
+// k_dog_zconv stored (`dsrc`, PD planes ahead) instead of being convolved here; the test,
+// the ring and the candidate records are the same code, so the same candidates.
+template <int KW, int BY, int PD, int BX, bool ONE, bool SL, bool FROMDOG = false>
 __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __restrict__ g12,
                                                          const float2* __restrict__ kz, float scale, int zc_len,
                                                          float* __restrict__ dog, float minv, int want,
-                                                         const PeakSink* __restrict__ sink, int xcd) {
+                                                         const PeakSink* __restrict__ sink, int xcd,
+                                                         const float* __restrict__ dsrc = nullptr) {
     constexpr int R = KW / 2;
-    constexpr int NW = KW + PD;
+    constexpr int NW = FROMDOG ? 12 : KW + PD;
     static_assert(NW % 4 == 0, "ring slots are compile-time: the unrolled rotation is whole ring turns");
     using Ring = DzRing<BY, BX>;
     __shared__ float Dr[Ring::kSize];
@@ -758,8 +764,8 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                        y <= ny - 2;
     // element offset of the source plane of every window index (mirror-single
     // extension, the tail repeating the last plane), for volumes the scalar path cannot take
-    __shared__ uint32_t zoff[SL ? 1 : kDzMaxLen];
-    if constexpr (!SL)
+    __shared__ uint32_t zoff[SL || FROMDOG ? 1 : kDzMaxLen];
+    if constexpr (!SL && !FROMDOG)
         for (int i = t; i < kDzMaxLen; i += BX * BY)
             zoff[i] = uint32_t(mirror32(qa - R + min(i, len - 1), nz)) * pstride;
     if (t < 4) nanq[t] = INT_MIN;   // (no plane)
@@ -767,6 +773,14 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     // unconditional loads (columns outside the volume read column 0): no branch merge,
     // so they stay in flight PD planes ahead
     const uint32_t plane_bytes = pstride * 8u;
+    // FROMDOG: DoG plane qa + i (the tail repeating the last plane)
+    const uint32_t dsrc_bytes = FROMDOG ? pstride * 4u : 0u;
+    auto ldd = [&](int i) -> float {
+        const int q = qa + min(i, qb - qa - 1);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(dsrc) + size_t(uint32_t(q)) * pstride, 0, int(dsrc_bytes), 0x00020000);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, int(col * 4u), 0, 0));
+    };
     auto ld = [&](int i) -> float2 {
         if constexpr (SL) {
             const int tz = qa - R + min(i, len - 1);
@@ -781,9 +795,13 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
     // step s: window = source planes s .. s + KW - 1 in slots (s + j) % NW, DoG plane
     // q = qa + s; the step count is padded to whole NW rotations (padded steps test and
     // store nothing), so the unrolled body has no exits
-    float2 w[NW];
+    float2 w[FROMDOG ? 1 : NW];
+    float wd[FROMDOG ? NW : 1];
 #pragma unroll
-    for (int p = 0; p < NW - 1; ++p) w[p] = ld(p);
+    for (int p = 0; p < NW - 1; ++p) {
+        if constexpr (FROMDOG) wd[p] = ldd(p);
+        else w[p] = ld(p);
+    }
     const int nsteps = (qb - qa + NW - 1) / NW * NW;
     float mnA = 0.f, mxA = 0.f, mnB = 0.f, mxB = 0.f, mnC = 0.f, mxC = 0.f, dB = 0.f, dC = 0.f;
     int nanhist = 0;   // bit k: the block's DoG plane q - k holds a NaN
@@ -799,6 +817,11 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
 #pragma unroll
         for (int ph = 0; ph < NW; ++ph) {
             const int st = sb + ph;
+            float dv;
+            if constexpr (FROMDOG) {
+                wd[(ph + NW - 1) % NW] = ldd(st + NW - 1);
+                dv = valid ? wd[ph % NW] : 0.0f;
+            } else {
             w[(ph + NW - 1) % NW] = ld(st + NW - 1);
             dg_v2 acc = {0.0f, 0.0f};
 #pragma unroll
@@ -807,9 +830,10 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                 const float2 k = kz[j <= R ? j : KW - 1 - j];
                 acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
             }
-            const float dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
+            dv = valid ? __fmul_rn(__fsub_rn(acc.y, acc.x), scale) : 0.0f;
+            }
             const int q = qa + st;
-            {   // the DoG store: a buffer store, dropped (out of range) unless owned
+            if constexpr (!FROMDOG) {   // the DoG store: a buffer store, dropped (out of range) unless owned
                 const bool st_ok = own && uint32_t(q - z0) < uint32_t(z1 - z0);
                 const int vo = int(st_ok ? col * 4u : 0x80000000u);
                 if constexpr (ONE) {
@@ -870,6 +894,233 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
                             make_int4(x, y | (sp << 30), zc, __float_as_int(fabsf(c)));
                     ccount += nb;
                 }
+            }
+        }
+    }
+    cand_flush(sink, cbuf[wv], ccount, nx, pstride);
+}
+
+// The split z stage, part 1: z Gaussians + DoG for every voxel, one thread per (x, y)
+// column of a chunk of zc_len planes (a wave = 64 consecutive x of one row), a register
+// window of KW planes + PD loaded ahead, rotating by unrolling; the DoG is stored for
+// every voxel and the 26-neighbour test runs afterwards over the stored image
+// (k_dog_z<..., FROMDOG>).  Columns are independent: no halo ring (the fused k_dog_z
+// convolved its box's ring too, 1.38x the loads and convolutions), no LDS, no barrier.
+// Same tap order and DoG expression as k_dog_z: the same bits.
+// (plane bytes nx * ny * 8 < 2^31: one buffer resource per source plane; ONE: the DoG
+// image below 2 GiB, one resource with the plane in the scalar offset)
+template <int KW, int PD, bool ONE, bool ONEG>
+__global__ __launch_bounds__(256) void k_dog_zconv(Dims3 d, const float2* __restrict__ g12,
+                                                   const float2* __restrict__ kz, float scale, int zc_len,
+                                                   float* __restrict__ dog) {
+    constexpr int R = KW / 2;
+    constexpr int NW = KW + PD;
+    const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
+    const int lane = int(threadIdx.x & 63);
+    const int gxw = (nx + 63) / 64;                                          // waves per row
+    const int wid = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
+    const int y = wid / gxw;
+    if (y >= ny) return;   // (wave-uniform; no barriers in this kernel)
+    const int x = (wid % gxw) * 64 + lane;
+    const bool valid = x < nx;
+    const int z0 = int(blockIdx.y) * zc_len, z1 = min(nz, z0 + zc_len);
+    const int len = z1 - z0 + KW - 1;   // source planes
+    const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
+    const uint32_t col = uint32_t(y) * uint32_t(nx) + uint32_t(valid ? x : nx - 1);
+    // G12 below 4 GiB (every 768^3-class view): one resource, the source plane's byte
+    // offset in the scalar offset (a resource per plane held 4 SGPRs per window slot)
+    const uint64_t g12_bytes = uint64_t(pstride) * uint64_t(nz) * 8u;
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(g12), 0, int(uint32_t(g12_bytes < 0xffffffffull ? g12_bytes : 0xffffffffull)), 0x00020000);
+    auto ld = [&](int i) -> float2 {
+        // mirror-single extension, one reflection (the host takes this kernel for nz > KW / 2)
+        const int tz = z0 - R + min(i, len - 1);
+        const int m = (nz - 1) - abs((nz - 1) - abs(tz));
+        if constexpr (ONEG)
+            return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rg, int(col * 8u),
+                                                                                   int(uint32_t(m) * pstride * 8u), 0));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float2*>(g12) + size_t(uint32_t(m)) * pstride, 0, int(pstride * 8u), 0x00020000);
+        return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, int(col * 8u), 0, 0));
+    };
+    float2 w[NW];
+#pragma unroll
+    for (int p = 0; p < NW - 1; ++p) w[p] = ld(p);
+    const int nsteps = (z1 - z0 + NW - 1) / NW * NW;   // padded to whole rotations (stores dropped)
+    const uint64_t dog_total = uint64_t(pstride) * uint64_t(nz) * 4u;
+    const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(dog, 0, ONE ? int(dog_total) : 0, 0x00020000);
+    for (int sb = 0; sb < nsteps; sb += NW) {
+#pragma unroll
+        for (int ph = 0; ph < NW; ++ph) {
+            const int st = sb + ph;
+            w[(ph + NW - 1) % NW] = ld(st + NW - 1);
+            dg_v2 acc = {0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {   // tap order kept
+                const float2 v = w[(ph + j) % NW];
+                const float2 k = kz[j <= R ? j : KW - 1 - j];
+                acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
+            }
+            const float dv = __fmul_rn(__fsub_rn(acc.y, acc.x), scale);
+            const int q = z0 + st;
+            const int vo = int(valid && q < z1 ? col * 4u : 0x80000000u);
+            if constexpr (ONE) {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rall, vo,
+                                                      int(uint32_t(min(q, nz - 1)) * pstride * 4u), 0);
+            } else {
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    dog + size_t(min(q, nz - 1)) * pstride, 0, int(pstride * 4u), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv), rd, vo, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // one load per step (hoisting them all held a rotation of VGPRs)
+        }
+    }
+}
+
+// The split z stage, part 2: the 26-neighbour test over the stored DoG image.  A wave =
+// 64 consecutive x (lanes 1..62 tested, lanes 0 and 63 their halo) x DPY rows per lane,
+// walking a chunk of zc_len centre planes: per plane each lane loads its column's DPY + 2
+// rows (PD planes ahead), the x neighbours come from DPP lane shifts, the y neighbours
+// from the lane's own rows, and the 3x3 min / max of the last two planes stay in
+// registers -- no LDS ring, no barrier (k_dog_z<FROMDOG> over the same image: 1.19 ms per
+// 768^3, this structure's serial step).  A centre plane next to a plane holding a NaN
+// (any loaded value of the wave) takes the reference's comparison loop over the image
+// for the wave (NaN compares false; min3 / max3 would drop it).
+__device__ __forceinline__ float dpp_from_left(float v) {    // lane i <- lane i - 1 (wave_shr:1)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {   // lane i <- lane i + 1 (wave_shl:1)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, false));
+}
+
+template <int DPY, int PD>
+__global__ __launch_bounds__(256) void k_dog_peaks(Dims3 d, const float* __restrict__ dog, int zc_len, float minv,
+                                                   int want, const PeakSink* __restrict__ sink) {
+    constexpr int NR = DPY + 2;    // rows loaded per plane
+    constexpr int NW = PD + 1;     // planes in the load ring
+    __shared__ int4 cbuf[4][kCandBuf];
+    const int lane = int(threadIdx.x & 63), wv = int(threadIdx.x >> 6);
+    const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
+    const int nsx = (nx - 2 + 61) / 62, nyb = (ny - 2 + DPY - 1) / DPY;
+    const int nzc = (nz - 2 + zc_len - 1) / zc_len;
+    const int wid = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+    if (wid >= nsx * nyb * nzc) return;   // (wave-uniform; no block barriers below)
+    const int sx = wid % nsx, yb = (wid / nsx) % nyb, zb = wid / (nsx * nyb);
+    const int x = sx * 62 + lane;                       // lane 0: the halo column x0 - 1
+    const bool xt = lane >= 1 && lane <= 62 && x <= nx - 2;
+    const int xl = min(x, nx - 1);
+    const int ybase = yb * DPY;                         // row r of the lane: y = ybase + r (r = 0: halo)
+    const int tlo = 1 + zb * zc_len, thi = min(nz - 1, tlo + zc_len);   // centre planes tested
+    const int qa = tlo - 1, qb = thi + 1;               // planes loaded
+    const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
+    const uint64_t total = uint64_t(pstride) * uint64_t(nz) * 4u;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(dog), 0, int(uint32_t(total < 0xffffffffull ? total : 0xffffffffull)), 0x00020000);
+    const uint32_t xoff = uint32_t(xl) * 4u;   // the only per-lane offset: rows and planes are scalar
+    auto ldp = [&](int i, float* v) {   // plane qa + i (the tail repeating the last plane)
+        const uint32_t po = uint32_t(qa + min(i, qb - qa - 1)) * pstride * 4u;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t so = po + uint32_t(min(ybase + r, ny - 1)) * uint32_t(nx) * 4u;
+            v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, int(xoff), int(so), 0));
+        }
+    };
+    float ring[NW][NR];
+#pragma unroll
+    for (int p = 0; p < NW - 1; ++p) ldp(p, ring[p]);
+    float mnA[DPY], mxA[DPY], mnB[DPY], mxB[DPY], cB[DPY];
+#pragma unroll
+    for (int r = 0; r < DPY; ++r) mnA[r] = mxA[r] = mnB[r] = mxB[r] = cB[r] = 0.0f;
+    int nanhist = 0;   // bit k: plane q - k held a NaN (any loaded value of the wave)
+    int ccount = 0;
+    const bool want_min = (want & 1) != 0, want_max = (want & 2) != 0;
+    const int nsteps = (qb - qa + NW - 1) / NW * NW;
+    for (int sb = 0; sb < nsteps; sb += NW) {
+#pragma unroll
+        for (int ph = 0; ph < NW; ++ph) {
+            const int st = sb + ph;
+            ldp(st + NW - 1, ring[(ph + NW - 1) % NW]);
+            const float* v = ring[ph % NW];   // plane q = qa + st
+            const int q = qa + st;
+            bool hasnan = false;
+            float xmn[NR], xmx[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                hasnan |= v[r] != v[r];
+                const float l = dpp_from_left(v[r]), rr = dpp_from_right(v[r]);
+                xmn[r] = dz_min3(l, v[r], rr);
+                xmx[r] = dz_max3(l, v[r], rr);
+            }
+            nanhist = ((nanhist << 1) | (__ballot(hasnan) != 0ull ? 1 : 0)) & 7;
+            float mnC[DPY], mxC[DPY];
+#pragma unroll
+            for (int r = 0; r < DPY; ++r) {
+                mnC[r] = dz_min3(xmn[r], xmn[r + 1], xmn[r + 2]);
+                mxC[r] = dz_max3(xmx[r], xmx[r + 1], xmx[r + 2]);
+            }
+            const int zc = q - 1;   // centre plane of the test
+            if (q < qb && zc >= tlo) {
+                // per row: bit r of fl = candidate, of mx = a MAX ("this mixup is intended",
+                // InteractiveIntegral.isSpecialPoint: every neighbour >= c is a MAX)
+                unsigned fl = 0u, mxb = 0u;
+#pragma unroll
+                for (int r = 0; r < DPY; ++r) {
+                    const float c = cB[r];
+                    const bool cand = xt && ybase + 1 + r <= ny - 2 && !(fabsf(c) < minv);
+                    const bool ge = dz_min3(mnA[r], mnB[r], mnC[r]) >= c;
+                    const bool le = dz_max3(mxA[r], mxB[r], mxC[r]) <= c;
+                    const bool is_max = cand && ge, is_min = cand && !ge && le;
+                    fl |= unsigned((is_max && want_max) || (is_min && want_min)) << r;
+                    mxb |= unsigned(is_max) << r;
+                }
+                if (nanhist != 0) {   // a NaN next to this plane: the comparison loop (rare)
+                    fl = 0u;
+                    mxb = 0u;
+#pragma unroll 1
+                    for (int r = 0; r < DPY; ++r) {
+                        const int y = ybase + 1 + r;
+                        const float c = dog[size_t(zc) * pstride + size_t(min(y, ny - 1)) * size_t(nx) + size_t(xl)];
+                        const bool cand = xt && y <= ny - 2 && !(fabsf(c) < minv);
+                        bool ge = true, le = true;
+                        if (cand) {
+#pragma unroll 1
+                            for (int k = 0; k < 27; ++k) {
+                                if (k == 13) continue;   // (the centre)
+                                const float u = dog[size_t(zc + k / 9 - 1) * pstride + size_t(y + (k / 3) % 3 - 1) * size_t(nx) +
+                                                    size_t(x + k % 3 - 1)];
+                                ge &= u >= c;
+                                le &= u <= c;
+                            }
+                        }
+                        const int spn = !cand ? 0 : ge ? 2 : le ? 1 : 0;
+                        fl |= unsigned((spn == 2 && want_max) || (spn == 1 && want_min)) << r;
+                        mxb |= unsigned(spn == 2) << r;
+                    }
+                }
+                if (__ballot(fl != 0u) != 0ull) {   // (rare: a few candidates per million voxels)
+#pragma unroll
+                    for (int r = 0; r < DPY; ++r) {
+                        const bool flag = ((fl >> r) & 1u) != 0u;
+                        const unsigned long long bal = __ballot(flag);
+                        if (bal == 0ull) continue;
+                        const int nb = __popcll(bal);
+                        if (ccount + nb > kCandBuf) {
+                            cand_flush(sink, cbuf[wv], ccount, nx, pstride);
+                            ccount = 0;
+                        }
+                        const int sp = ((mxb >> r) & 1u) ? 2 : 1;
+                        if (flag)
+                            cbuf[wv][ccount + __popcll(bal & ((1ull << lane) - 1ull))] =
+                                make_int4(x, (ybase + 1 + r) | (sp << 30), zc, __float_as_int(fabsf(cB[r])));
+                        ccount += nb;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < DPY; ++r) {
+                mnA[r] = mnB[r]; mxA[r] = mxB[r];
+                mnB[r] = mnC[r]; mxB[r] = mxC[r];
+                cB[r] = v[r + 1];
             }
         }
     }
@@ -1426,6 +1677,16 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, bx - 2))),
                   unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, bz_y - 2))), unsigned(ceil_div(d.nz, zc)));
     bool store_dog = need_dog;
+    // the split z stage (default): k_dog_zconv stores the DoG of every voxel, then k_dog_z
+    // tests over the stored image (SPIMDECON_DOG_SPLIT=0: the fused k_dog_z); a candidate
+    // overflow reruns the test pass only
+    const bool split = fused && dog_env("SPIMDECON_DOG_SPLIT", 1) != 0 && d.nx * d.ny * 8 < (int64_t(1) << 31) &&
+                       d.nz > K / 2;   // (k_dog_zconv's one-reflection plane index)
+    const int zc1 = std::max(1, dog_env("SPIMDECON_DOG_ZC_CHUNK", 256));
+    if (split && !dogp) {
+        grow(w.dog, size_t(n));
+        dogp = w.dog.p;
+    }
     if (fused) {
         grow(w.g12, size_t(n));
 #define SD_DOGXY(KV)                                                                                        \
@@ -1434,6 +1695,17 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
+        if (split) {
+            const int64_t waves = ceil_div(d.nx, int64_t(64)) * d.ny;
+            const dim3 gc(unsigned(ceil_div(waves, int64_t(4))), unsigned(ceil_div(d.nz, int64_t(zc1))));
+            const bool one1 = uint64_t(n) * 4u < 0x80000000ull, oneg = uint64_t(n) * 8u < 0xffffffffull;
+#define SD_DOGZC(KV) if (one1 && oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, true, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else if (oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, false, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, false, false>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp);
+            if (K == 7) { SD_DOGZC(7) } else if (K == 15) { SD_DOGZC(15) } else { SD_DOGZC(31) }
+#undef SD_DOGZC
+            SD_HIP(hipGetLastError());
+        }
     } else {
         // Gaussians of 63 / 127 taps: the separate passes, then a candidate pass over the DoG
         grow(w.tmp_a, size_t(n));
@@ -1457,7 +1729,26 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         grow(w.recs, cap);
         SD_HIP(hipMemsetAsync(w.count.p, 0, sizeof(unsigned), s));
         const PeakSink pk{min_peak, wmin, wmax, T, w.keys.p, w.vals.p, w.recs.p, w.count.p, cap};
-        if (fused) {
+        if (split) {
+            grow(w.sink, 1);
+            SD_HIP(hipMemcpyAsync(w.sink.p, &pk, sizeof(pk), hipMemcpyHostToDevice, s));   // (synchronised below)
+            const int want = wmin | (wmax << 1);
+            if (dog_env("SPIMDECON_DOG_PEAKS_RING", 0)) {   // (A/B: the ring test of k_dog_z over the image)
+#define SD_DOGT4(KV, BYV) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, 64, true, true, true>), gz, dim3(64 * BYV), 0, s, d, w.g12.p, kp2(2), kinv, zc, nullptr, min_peak, want, w.sink.p, xcd, dogp);
+#define SD_DOGT(KV) if (bz_y == 16) { SD_DOGT4(KV, 16) } else { SD_DOGT4(KV, 8) }
+                if (K == 7) { SD_DOGT(7) } else if (K == 15) { SD_DOGT(15) } else { SD_DOGT(31) }
+#undef SD_DOGT
+#undef SD_DOGT4
+            } else if (d.nx >= 3 && d.ny >= 3 && d.nz >= 3) {   // (else no voxel has 26 neighbours)
+                const int zcp = std::max(1, dog_env("SPIMDECON_DOG_PEAKS_ZC", 64));
+                const int dpy = dog_env("SPIMDECON_DOG_PEAKS_Y", kDpkY) == 8 ? 8 : 4;
+                const int64_t nwave = ceil_div(d.nx - 2, int64_t(62)) * ceil_div(d.ny - 2, int64_t(dpy)) *
+                                      ceil_div(d.nz - 2, int64_t(zcp));
+                const dim3 gp(unsigned(ceil_div(nwave, int64_t(4))));
+                if (dpy == 8) hipLaunchKernelGGL((k_dog_peaks<8, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p);
+                else hipLaunchKernelGGL((k_dog_peaks<4, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p);
+            }
+        } else if (fused) {
             float* dst = store_dog ? dogp : nullptr;
             grow(w.sink, 1);
             SD_HIP(hipMemcpyAsync(w.sink.p, &pk, sizeof(pk), hipMemcpyHostToDevice, s));   // (synchronised below)

@@ -1,0 +1,137 @@
+// zpattern_bench.hip -- HBM rate of the z pass's access pattern, without its compute.
+// A spectrum of P planes x E complex elements (540^3 engine: P = 536, E = 540 * 272);
+// a tile = SEG consecutive elements, all planes (the z pass reads and rewrites every
+// plane's SEG * 8-byte segment of its tile).  Every block walks its tiles; its waves
+// read 1-KiB pieces (1024 / (SEG * 8) planes per piece, or part of a plane for
+// SEG > 128), DEPTH pieces in flight per wave, and write each back (+1).  The layout
+// variant "brick" stores planes in groups of ZB: [P / ZB][E][ZB], so a tile's ZB
+// planes are one contiguous ZB * SEG * 8-byte run (what a z-brick layout would give).
+// usage: zpattern_bench  (prints one line per variant)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+            std::exit(1);                                                                       \
+        }                                                                                       \
+    } while (0)
+
+// piece j of tile t: plane-major pieces.  Plane layout: element (p, e) at p * E + e
+// (planar) or (p / ZB) * E * ZB + e * ZB + p % ZB (brick, SEG elements per plane run
+// become SEG * ZB contiguous elements per plane group).
+template <int DEPTH>
+__global__ __launch_bounds__(512) void k_pattern(float4* buf, long E, int P, int seg, int zb, int stagger) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const long ntiles = E / seg;
+    const int bytes_tile_plane = seg * 8;                  // bytes of one plane's segment
+    const long tile_bytes = long(bytes_tile_plane) * P;    // bytes of a tile
+    const int npieces = int(tile_bytes / 1024);
+    const int lseg = __builtin_ctz(bytes_tile_plane);
+    const int lzb = zb > 1 ? __builtin_ctz(zb) : 0;
+    for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int stag = stagger ? int((uint32_t(blockIdx.x) * 2654435761u) % uint32_t(npieces)) : 0;
+        for (int j0 = wave * DEPTH; j0 < npieces; j0 += 8 * DEPTH) {
+            float4 v[DEPTH];
+            long off[DEPTH];
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+                int j = j0 + d;
+                off[d] = -1;
+                if (j < npieces) {
+                    j += stag;
+                    if (j >= npieces) j -= npieces;
+                    // byte b of the tile: 16 * (64 j + lane); segment sizes are powers of two
+                    const int b = (j * 64 + lane) * 16;
+                    if (zb <= 1) {
+                        const int p = b >> lseg, eb = b & (bytes_tile_plane - 1);
+                        off[d] = (long(p) * E * 8 + tile * bytes_tile_plane + eb) >> 4;
+                    } else {
+                        const int g = b >> (lseg + lzb), eb = b & ((bytes_tile_plane << lzb) - 1);
+                        off[d] = (long(g) * E * 8 * zb + (tile * bytes_tile_plane << lzb) + eb) >> 4;
+                    }
+                    v[d] = buf[off[d]];
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d)
+                if (off[d] >= 0) {
+                    float4 w = v[d];
+                    w.x += 1.0f;
+                    buf[off[d]] = w;
+                }
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) void k_stream(float4* buf, long n) {
+    for (long i = blockIdx.x * 512L + threadIdx.x; i < n; i += long(gridDim.x) * 512) {
+        float4 w = buf[i];
+        w.x += 1.0f;
+        buf[i] = w;
+    }
+}
+
+int main() {
+    const int P = 536;
+    const long E = 540L * 272;   // multiple of every SEG below
+    const size_t bytes = size_t(P) * E * 8;
+    float4* buf;
+    CK(hipMalloc(&buf, bytes));
+    CK(hipMemset(buf, 0, bytes));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    struct V { int seg, zb, stag, grid, depth; };
+    std::vector<V> vs;
+    for (int seg : {16, 32, 64})
+        for (int stag : {1, 0})
+            for (int grid : {256, 1024})
+                vs.push_back({seg, 1, stag, grid, 4});
+    for (int seg : {16, 32})
+        for (int zb : {4, 8})
+            for (int grid : {256, 1024})
+                vs.push_back({seg, zb, 1, grid, 4});
+    vs.push_back({32, 1, 1, 256, 8});
+    vs.push_back({32, 1, 1, 256, 2});
+    std::printf("seg_bytes zbrick stagger grid depth ms TB/s(read+write)\n");
+    for (const V& v : vs) {
+        auto launch = [&] {
+            if (v.depth == 8) hipLaunchKernelGGL(k_pattern<8>, dim3(v.grid), dim3(512), 0, 0, buf, E, P, v.seg, v.zb, v.stag);
+            else if (v.depth == 2) hipLaunchKernelGGL(k_pattern<2>, dim3(v.grid), dim3(512), 0, 0, buf, E, P, v.seg, v.zb, v.stag);
+            else hipLaunchKernelGGL(k_pattern<4>, dim3(v.grid), dim3(512), 0, 0, buf, E, P, v.seg, v.zb, v.stag);
+        };
+        launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 10;
+        CK(hipEventRecord(a));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ms /= reps;
+        std::printf("%d %d %d %d %d %.4f %.3f\n", v.seg * 8, v.zb, v.stag, v.grid, v.depth, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
+        std::fflush(stdout);
+    }
+    for (int grid : {1024, 4096}) {   // contiguous reference
+        hipLaunchKernelGGL(k_stream, dim3(grid), dim3(512), 0, 0, buf, long(bytes / 16));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        for (int r = 0; r < 10; ++r) hipLaunchKernelGGL(k_stream, dim3(grid), dim3(512), 0, 0, buf, long(bytes / 16));
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ms /= 10;
+        std::printf("contiguous grid %d %.4f ms %.3f TB/s\n", grid, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
+    }
+    CK(hipFree(buf));
+    return 0;
+}
