@@ -365,7 +365,14 @@ constexpr int kDzPD = SPIMDECON_DZ_PD;
                              // (a step computes in ~350 cycles; a load takes thousands)
 constexpr int kDzChunk = 128; // DoG planes per block (the window adds KW - 1 + 2 loads; 64: 2.46 vs 2.35 ms)
 constexpr int kDzMaxLen = 512;
-constexpr int kDpkY = 4;    // k_dog_peaks: rows per lane
+constexpr int kDpkY = 4;
+#ifndef SPIMDECON_DZC_PD
+#define SPIMDECON_DZC_PD 9
+#endif
+#ifndef SPIMDECON_DZC_ILV
+#define SPIMDECON_DZC_ILV 0
+#endif
+constexpr int kDzcPD = SPIMDECON_DZC_PD;   // k_dog_zconv: planes loaded ahead    // k_dog_peaks: rows per lane
 constexpr int kDpkPD = 2;   // k_dog_peaks: planes loaded ahead   // k_dog_z plane-offset table: chunk + 2 + KW - 1 + PD entries
 
 __device__ __forceinline__ int mirror32(int i, int n) {
@@ -960,6 +967,7 @@ __global__ __launch_bounds__(256) void k_dog_zconv(Dims3 d, const float2* __rest
                 const float2 v = w[(ph + j) % NW];
                 const float2 k = kz[j <= R ? j : KW - 1 - j];
                 acc = acc + dg_v2{v.x, v.y} * dg_v2{k.x, k.y};
+                if (SPIMDECON_DZC_ILV) __builtin_amdgcn_sched_barrier(0);
             }
             const float dv = __fmul_rn(__fsub_rn(acc.y, acc.x), scale);
             const int q = z0 + st;
@@ -995,7 +1003,7 @@ __device__ __forceinline__ float dpp_from_right(float v) {   // lane i <- lane i
 
 template <int DPY, int PD>
 __global__ __launch_bounds__(256) void k_dog_peaks(Dims3 d, const float* __restrict__ dog, int zc_len, float minv,
-                                                   int want, const PeakSink* __restrict__ sink) {
+                                                   int want, const PeakSink* __restrict__ sink, int xcd) {
     constexpr int NR = DPY + 2;    // rows loaded per plane
     constexpr int NW = PD + 1;     // planes in the load ring
     __shared__ int4 cbuf[4][kCandBuf];
@@ -1003,7 +1011,14 @@ __global__ __launch_bounds__(256) void k_dog_peaks(Dims3 d, const float* __restr
     const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
     const int nsx = (nx - 2 + 61) / 62, nyb = (ny - 2 + DPY - 1) / DPY;
     const int nzc = (nz - 2 + zc_len - 1) / zc_len;
-    const int wid = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+    // xcd: blocks go round-robin to the 8 XCDs; the logical block index gives each XCD a
+    // contiguous range, so the y-neighbour waves sharing a halo row run on one L2
+    int lb = int(blockIdx.x);
+    if (xcd) {
+        const unsigned b = blockIdx.x, k = b & 7u, j = b >> 3, q = gridDim.x >> 3, r = gridDim.x & 7u;
+        lb = int(k * q + min(k, r) + j);
+    }
+    const int wid = __builtin_amdgcn_readfirstlane(lb * 4 + wv);
     if (wid >= nsx * nyb * nzc) return;   // (wave-uniform; no block barriers below)
     const int sx = wid % nsx, yb = (wid / nsx) % nyb, zb = wid / (nsx * nyb);
     const int x = sx * 62 + lane;                       // lane 0: the halo column x0 - 1
@@ -1699,9 +1714,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
             const int64_t waves = ceil_div(d.nx, int64_t(64)) * d.ny;
             const dim3 gc(unsigned(ceil_div(waves, int64_t(4))), unsigned(ceil_div(d.nz, int64_t(zc1))));
             const bool one1 = uint64_t(n) * 4u < 0x80000000ull, oneg = uint64_t(n) * 8u < 0xffffffffull;
-#define SD_DOGZC(KV) if (one1 && oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, true, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
-            else if (oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, false, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
-            else hipLaunchKernelGGL((k_dog_zconv<KV, kDzPD, false, false>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp);
+#define SD_DOGZC(KV) if (one1 && oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, true, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else if (oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, false>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp);
             if (K == 7) { SD_DOGZC(7) } else if (K == 15) { SD_DOGZC(15) } else { SD_DOGZC(31) }
 #undef SD_DOGZC
             SD_HIP(hipGetLastError());
@@ -1745,8 +1760,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
                 const int64_t nwave = ceil_div(d.nx - 2, int64_t(62)) * ceil_div(d.ny - 2, int64_t(dpy)) *
                                       ceil_div(d.nz - 2, int64_t(zcp));
                 const dim3 gp(unsigned(ceil_div(nwave, int64_t(4))));
-                if (dpy == 8) hipLaunchKernelGGL((k_dog_peaks<8, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p);
-                else hipLaunchKernelGGL((k_dog_peaks<4, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p);
+                const int pxcd = dog_env("SPIMDECON_DOG_PEAKS_XCD", 1);
+                if (dpy == 8) hipLaunchKernelGGL((k_dog_peaks<8, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p, pxcd);
+                else hipLaunchKernelGGL((k_dog_peaks<4, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p, pxcd);
             }
         } else if (fused) {
             float* dst = store_dog ? dogp : nullptr;
