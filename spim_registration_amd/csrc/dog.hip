@@ -429,7 +429,7 @@ __device__ __forceinline__ DzBox xcd_box(bool xcd) {
     return {int(l % gx), int((l / gx) % gy), int(l / (gx * gy))};
 }
 
-template <int KW, int TY>
+template <int KW, int TY, bool BUF = true>
 __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
                                                 const float* __restrict__ mm, int xcd) {
@@ -472,6 +472,14 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
         y0 = ((tile / gx) % gy) * TY;
         plane = uint32_t(tile / (gx * gy)) * uint32_t(ny) * uint32_t(nx);
     };
+    // BUF (image below 4 GiB): buffer loads, the lane's row offset in a VGPR and the
+    // pass offset RPT * e * nx in the scalar offset (no per-load address arithmetic; rows
+    // past the tile load in range or return 0 and are never staged); y mirror indices by
+    // one reflection when ny > R (the modulo of mirror32 cost ~15 VALU per staged value
+    // on the border tiles)
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(in), 0, int(uint32_t(BUF ? uint64_t(d.nx * d.ny * d.nz) * 4u : 0u)), 0x00020000);
+    const bool yrefl = ny > R;
     auto stage_loads = [&](int tile, float* v) {
         int x0, y0;
         uint32_t plane;
@@ -479,14 +487,27 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
         const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && y0 - R >= 0 && y0 - R + IH <= ny;
         if (inside) {
             const uint32_t base = plane + uint32_t(y0 - R) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
+            if constexpr (BUF) {
+                const uint32_t vo = (base + uint32_t(r0) * uint32_t(nx)) * 4u;
 #pragma unroll
-            for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
+                for (int e = 0; e < NE; ++e)
+                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         rin, int(vo), int(uint32_t(RPT * e) * uint32_t(nx) * 4u), 0));
+            } else {
+#pragma unroll
+                for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
+            }
         } else {
             const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
-                const int row = min(r0 + RPT * e, IH - 1);
-                v[e] = in[gxo + uint32_t(mirror32(y0 - R + row, ny)) * uint32_t(nx)];
+                const int yy = y0 - R + min(r0 + RPT * e, IH - 1);
+                const int my = yrefl ? (ny - 1) - abs((ny - 1) - abs(yy)) : mirror32(yy, ny);
+                if constexpr (BUF)
+                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         rin, int((gxo + uint32_t(my) * uint32_t(nx)) * 4u), 0, 0));
+                else
+                    v[e] = in[gxo + uint32_t(my) * uint32_t(nx)];
             }
         }
     };
@@ -1704,9 +1725,11 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     }
     if (fused) {
         grow(w.g12, size_t(n));
+        const bool xbuf = uint64_t(n) * 4u < 0xffffffffull && dog_env("SPIMDECON_DOG_XY_BUF", 1) != 0;
 #define SD_DOGXY(KV)                                                                                        \
-        if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, 32>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy);
+        if (ty == 48 && xbuf) hipLaunchKernelGGL((k_dog_xy<KV, 48, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
+        else if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, 32, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy);
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
