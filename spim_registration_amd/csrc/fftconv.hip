@@ -525,11 +525,12 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     static const int np_env = [] {  // row pairs per tile, SPIMDECON_XTP=8|16 for A/B runs
         const char* e = std::getenv("SPIMDECON_XTP");
         const int v = e ? std::atoi(e) : 0;
-        return v == 8 || v == 16 ? v : 0;
+        return v == 4 || v == 8 || v == 16 ? v : 0;
     }();
     // 8 pairs per tile (one tile per block): quotient 0.40 vs 0.43 ms with 16 pairs
     // and 0.45 with 4, update 0.52 vs 0.58 / 0.54 ms; at L = 1050 quotient 0.90 vs 1.05 ms
-    const int np = np_env ? np_env : 8;
+    const int L0 = int(p.g.Mx);
+    const int np = np_env == 4 && L0 != 1050 && L0 != 800 ? 8 : (np_env ? np_env : 8);
     XArgs b;
     if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
@@ -556,6 +557,20 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
         hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, NP, TRv>), dim3(grid), dim3(NP * TRv), lds, s, b); \
         done = true;                                                                                      \
     }
+    // 4 row pairs per tile for the long lengths (SPIMDECON_XTP=4, A/B): twice the
+    // independent blocks per CU at the same occupancy (the twiddle table leaves the LDS)
+#define SD_XT4(SV, A, B, TK)                                                                                \
+    if (!done && np == 4 && sv == SV && L == (A) * (B) && tik == TK) {                                    \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, 4, SD_2F_TR(A, B)>), \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                \
+        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, 4, SD_2F_TR(A, B)>), dim3(grid), dim3(4 * SD_2F_TR(A, B)), lds, s, b); \
+        done = true;                                                                                      \
+    }
+#define SD_XT4S(A, B) SD_XT4(0, A, B, false) SD_XT4(1, A, B, false) \
+    if constexpr (MODE == XM_UPDATE) { SD_XT4(0, A, B, true) SD_XT4(1, A, B, true) }
+    SD_XT4S(30, 35) SD_XT4S(25, 32)
+#undef SD_XT4S
+#undef SD_XT4
 #define SD_XT_N(A, B, NP) \
     SD_XT(0, A, B, false, NP) SD_XT(1, A, B, false, NP) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true, NP) SD_XT(1, A, B, true, NP) }
 #define SD_XT_S(A, B) if constexpr ((A) * (B) <= 1204) { SD_XT_N(A, B, 16) } SD_XT_N(A, B, 8)
