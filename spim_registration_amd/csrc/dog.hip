@@ -1716,8 +1716,10 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     // the split z stage (default): k_dog_zconv stores the DoG of every voxel, then k_dog_z
     // tests over the stored image (SPIMDECON_DOG_SPLIT=0: the fused k_dog_z); a candidate
     // overflow reruns the test pass only
+    // (k_dog_zconv's one-reflection plane index needs nz > K / 2; k_dog_peaks addresses the
+    // DoG image through one buffer resource with 32-bit plane offsets: below 4 GiB)
     const bool split = fused && dog_env("SPIMDECON_DOG_SPLIT", 1) != 0 && d.nx * d.ny * 8 < (int64_t(1) << 31) &&
-                       d.nz > K / 2;   // (k_dog_zconv's one-reflection plane index)
+                       d.nz > K / 2 && uint64_t(n) * 4u < 0xffffffffull;
     const int zc1 = std::max(1, dog_env("SPIMDECON_DOG_ZC_CHUNK", 256));
     if (split && !dogp) {
         grow(w.dog, size_t(n));
