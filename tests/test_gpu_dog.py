@@ -189,6 +189,28 @@ def test_dog_nan_planes_take_the_comparison_loop(gpu):
     assert [(q[4], q[5]) for q in pk] == [(e[4], e[5]) for e in exp]
 
 
+@pytest.mark.parametrize("sigma", [1.0, 1.8, 4.0])
+def test_dog_split_and_fused_z_stages_agree(gpu, sigma, monkeypatch):
+    """The split z stage (k_dog_zconv + k_dog_peaks, the default) and the fused
+    k_dog_z (SPIMDECON_DOG_SPLIT=0) give the same DoG image and the same ordered
+    candidate list, NaN planes (the comparison loop) and several row / plane
+    chunks included; 7 / 15 / 31 taps."""
+    img = bead_stack(shape=(150, 70, 131), cid=24)
+    img[70, 30, 64] = np.nan
+    img[3, 68, 2] = np.nan
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("SPIMDECON_DOG_SPLIT", split)
+        pk = dog.simple_peaks(img, sigma=sigma, threshold=0.001, find_min=True, find_max=True,
+                              min_intensity=0.0, max_intensity=4000.0, ij_threads=5)
+        _, d = dog.compute(img, sigma=sigma, threshold=0.001, min_intensity=0.0, max_intensity=4000.0,
+                           return_dog=True)
+        out[split] = (pk, d)
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    assert len(out["1"][0]) > 10
+    assert out["1"][0] == out["0"][0]
+
+
 def test_dog_workspace_release_and_reuse(gpu):
     """The per-device workspace grows to the largest view and is reused; releasing it
     and calling again gives the same result."""
