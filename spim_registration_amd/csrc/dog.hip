@@ -432,7 +432,7 @@ __device__ __forceinline__ DzBox xcd_box(bool xcd) {
 template <int KW, int TY, bool BUF = true>
 __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
-                                                const float* __restrict__ mm, int xcd) {
+                                                const float* __restrict__ mm, int xcd, int mm_exact) {
     constexpr int R = KW / 2;
     constexpr int IW = kDxyTX + KW - 1;          // staged input columns
     constexpr int IP = dxy_in_pitch(IW);         // pitch (see dxy_in_pitch)
@@ -458,6 +458,12 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
         rd = __frcp_rn(diff);
         if (!(fabsf(diff) >= 0x1p-48f && fabsf(diff) <= 0x1p48f)) rd = 0.0f;   // (division only)
     }
+    // mm_exact: mn / mx are the image's own min / max (k_minmax, not caller-given), so
+    // every finite value has mn <= v <= mx and a = v - mn lies in [0, diff]; with
+    // |mn| >= 2^-20 a non-zero a is at least the float spacing just below 2^-20 (2^-44), and
+    // a = 0 is +0: every a is in the reciprocal path's exact range (NaN stays NaN either
+    // way), so the per-value range check is skipped for the whole launch
+    const bool allfast = norm && mm_exact != 0 && rd != 0.0f && fabsf(mn) >= 0x1p-20f;
     // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
     // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
     // load.  Tiles whose staged box lies inside the volume (all but the outer ring of
@@ -534,10 +540,12 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
                 v[e] = __fsub_rn(v[e], mn);
-                const float aa = fabsf(v[e]);
-                bad |= !((aa >= 0x1p-48f && aa <= 0x1p48f) || __float_as_uint(v[e]) == 0u);   // (+0 only)
+                if (!allfast) {
+                    const float aa = fabsf(v[e]);
+                    bad |= !((aa >= 0x1p-48f && aa <= 0x1p48f) || __float_as_uint(v[e]) == 0u);   // (+0 only)
+                }
             }
-            if (!__any(bad)) {
+            if (allfast || !__any(bad)) {
 #pragma unroll
                 for (int e = 0; e < NE; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
             } else {
@@ -1728,10 +1736,11 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     if (fused) {
         grow(w.g12, size_t(n));
         const bool xbuf = uint64_t(n) * 4u < 0xffffffffull && dog_env("SPIMDECON_DOG_XY_BUF", 1) != 0;
+        const int mmx = !use_given && X
 #define SD_DOGXY(KV)                                                                                        \
-        if (ty == 48 && xbuf) hipLaunchKernelGGL((k_dog_xy<KV, 48, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
-        else if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, 32, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy);
+        if (ty == 48 && xbuf) hipLaunchKernelGGL((k_dog_xy<KV, 48, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
+        else if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, 32, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
