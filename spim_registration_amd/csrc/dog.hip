@@ -1736,9 +1736,9 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     if (fused) {
         grow(w.g12, size_t(n));
         const bool xbuf = uint64_t(n) * 4u < 0xffffffffull && dog_env("SPIMDECON_DOG_XY_BUF", 1) != 0;
-        // (k_minmax's own range: the per-value range check is skipped; SPIMDECON_DOG_MM_EXACT=1,
-        // off by default until measured)
-        const int mmx = !use_given && dog_env("SPIMDECON_DOG_MM_EXACT", 0) != 0 ? 1 : 0;
+        // (k_minmax's own range: the per-value range check is skipped; SPIMDECON_DOG_MM_EXACT=0
+        // keeps it -- 1.52-1.62 vs 1.66 ms per 768^3, bit-exact, gpu_r3z11.sh)
+        const int mmx = !use_given && dog_env("SPIMDECON_DOG_MM_EXACT", 1) != 0 ? 1 : 0;
 #define SD_DOGXY(KV)                                                                                        \
         if (ty == 48 && xbuf) hipLaunchKernelGGL((k_dog_xy<KV, 48, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
         else if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
