@@ -182,6 +182,15 @@ int mvd_comm_unique_id(char* out128);
 /* global [z0, z1) of part `idx` of `nparts` over nz planes (balanced split) */
 int mvd_slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1);
 
+/* The halo transfers of one slab (nz interior planes, Mz padded planes, cz halo planes,
+ * plane_elems floats per padded plane), as float offsets into its spectrum buffer:
+ * out5 = {send_lo, recv_lo, send_hi, recv_hi, count}.  To / from the lower neighbour:
+ * send [0, cz), receive into [Mz - cz, Mz); to / from the upper one: send [nz - cz, nz),
+ * receive into [nz, nz + cz).  The one helper behind the local slab copies, the device-
+ * group peer pulls and the RCCL send / recv (MVDeconFFT.java:424-446 runs the blocks of
+ * one volume on several devices; here neighbouring slabs trade halo planes). */
+int mvd_halo_plan(int64_t nz, int64_t Mz, int cz, int64_t plane_elems, int64_t* out5);
+
 int  mvd_create(const mvd_params* params, mvd_session** out);
 /* One session over several GPUs of this process -- the reference's
  * MVDeconFFT(img, weight, kernel, factory, int[] deviceList, ...) driven from one
@@ -340,7 +349,11 @@ int spim_save_interest_points(const char* base_dir, const char* file, const spim
                               const int32_t* ids, int64_t n);
 int spim_load_interest_points(const char* base_dir, const char* file, spim_interest_point* out,
                               int32_t* ids, int64_t max_out, int64_t* nout);
-/* Java Double.toString of d into out (cap bytes incl. the terminator) */
+/* Java Double.toString of d into out (cap bytes incl. the terminator), in the form of
+ * the selected Java version (also used by spim_save_interest_points): 8 (default; Fiji
+ * runs Java 8: sun.misc.FloatingDecimal, e.g. 2.0E23 -> "1.9999999999999998E23") or 19
+ * (JDK 19+: the shortest decimal that round-trips, "2.0E23").  Process-wide. */
+int spim_set_java_version(int jdk);
 int spim_java_double_to_string(double d, char* out, int cap);
 
 /* ======================================================================

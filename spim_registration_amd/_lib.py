@@ -105,6 +105,7 @@ SIGNATURES = {
     "mvd_params_default": (None, [C.POINTER(MvdParams)]),
     "mvd_comm_unique_id": (C.c_int, [C.c_char_p]),
     "mvd_slab_range": (C.c_int, [_i64, C.c_int, C.c_int, _pi64, _pi64]),
+    "mvd_halo_plan": (C.c_int, [_i64, _i64, C.c_int, _i64, _pi64]),
     "mvd_create": (C.c_int, [C.POINTER(MvdParams), C.POINTER(C.c_void_p)]),
     "mvd_create_devices": (C.c_int, [_pi, C.c_int, C.POINTER(MvdParams), C.POINTER(C.c_void_p)]),
     "mvd_destroy": (None, [C.c_void_p]),
@@ -143,6 +144,7 @@ SIGNATURES = {
     "spim_load_interest_points": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(InterestPointC),
                                             C.POINTER(C.c_int32), C.c_int64, _pi64]),
     "spim_java_double_to_string": (C.c_int, [C.c_double, C.c_char_p, C.c_int]),
+    "spim_set_java_version": (C.c_int, [C.c_int]),
     "convolutionCPU": (C.c_int, [_pf, _pf, _pf, _pf, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_float]),
     "spim_input_params_default": (None, [C.POINTER(InputParams)]),

@@ -192,6 +192,18 @@ int mvd_slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1) {
     });
 }
 
+int mvd_halo_plan(int64_t nz, int64_t Mz, int cz, int64_t plane_elems, int64_t* out5) {
+    return guarded([&] {
+        SD_CHECK(out5, SPIMDECON_ERR_ARG, "null argument");
+        const HaloPlan h = halo_plan(nz, Mz, cz, plane_elems);
+        out5[0] = h.send_lo;
+        out5[1] = h.recv_lo;
+        out5[2] = h.send_hi;
+        out5[3] = h.recv_hi;
+        out5[4] = h.count;
+    });
+}
+
 int mvd_create(const mvd_params* params, mvd_session** out) {
     return guarded([&] {
         SD_CHECK(params && out, SPIMDECON_ERR_ARG, "null argument");

@@ -25,6 +25,17 @@ void slab_range(int64_t nz, int nparts, int idx, int64_t* z0, int64_t* z1) {
     *z1 = *z0 + base + (idx < rem ? 1 : 0);
 }
 
+HaloPlan halo_plan(int64_t nz, int64_t Mz, int64_t cz, int64_t plane) {
+    SD_CHECK(cz >= 0 && nz >= cz && Mz >= nz + 2 * cz && plane > 0, SPIMDECON_ERR_ARG, "bad halo geometry");
+    HaloPlan h;
+    h.send_lo = 0;
+    h.recv_lo = (Mz - cz) * plane;
+    h.send_hi = (nz - cz) * plane;
+    h.recv_hi = nz * plane;
+    h.count = cz * plane;
+    return h;
+}
+
 void HostBarrier::wait() {
     std::unique_lock<std::mutex> lk(mu_);
     if (aborted_) fail(SPIMDECON_ERR_STATE, "device group aborted");
@@ -87,9 +98,13 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
     if (p0.fft_backend == 0 && auto_slabs && p0.local_slabs >= 1) {
         auto needed = [&](const mvd_params& q, int ls) {
             const int hal[3] = {std::max(q.halo[0], 16), std::max(q.halo[1], 16), std::max(q.halo[2], 16)};
-            while (ls < q.dims[2] && !engine_slab_fits(q.dims[0], q.dims[1], ceil_div(q.dims[2], int64_t(G) * ls),
-                                                       hal, q.fft_pad_policy))
-                ++ls;
+            auto fits = [&](int64_t nzs) {
+                return engine_slab_fits(q.dims[0], q.dims[1], nzs, hal, q.fft_pad_policy);
+            };
+            // when even one-plane slabs are past the fast passes' offsets no split helps:
+            // keep the caller's slab count (the Stockham passes run it, as before)
+            if (!fits(1)) return ls;
+            while (int64_t(G) * ls < q.dims[2] && !fits(ceil_div(q.dims[2], int64_t(G) * ls))) ++ls;
             return ls;
         };
         int ls = needed(p_, p0.local_slabs);
@@ -575,38 +590,36 @@ void Session::exchange(bool which, hipStream_t st) {
     if (S == 1 && p_.nranks == 1) return;
     const int cz = halo_[2];
     if (cz <= 0) return;
-    const size_t plane = plane_floats();
+    const int64_t plane = int64_t(plane_floats());
     auto get = [&](SlabState& sl) { return buf_ptr(sl, which, backend_); };
+    auto hp = [&](const SlabState& sl) { return halo_plan(sl.g.nz, sl.g.Mz, cz, plane); };
     tstart(5, st);
-    const size_t bytes = size_t(cz) * plane * sizeof(float);
+    const size_t bytes = size_t(cz) * size_t(plane) * sizeof(float);
     for (int s = 1; s < S; ++s) {
         SlabState& lo = slabs_[s - 1];
         SlabState& hi = slabs_[s];
-        // hi's first cz planes -> lo's upper halo [nz_lo, nz_lo + cz)
-        SD_HIP(hipMemcpyAsync(get(lo) + size_t(lo.g.nz) * plane, get(hi), bytes,
-                              hipMemcpyDeviceToDevice, st));
-        // lo's last cz planes -> hi's lower halo [Mz_hi - cz, Mz_hi)
-        SD_HIP(hipMemcpyAsync(get(hi) + size_t(hi.g.Mz - cz) * plane,
-                              get(lo) + size_t(lo.g.nz - cz) * plane, bytes,
-                              hipMemcpyDeviceToDevice, st));
+        const HaloPlan hl = hp(lo), hh = hp(hi);
+        // hi's first cz planes -> lo's upper halo
+        SD_HIP(hipMemcpyAsync(get(lo) + hl.recv_hi, get(hi) + hh.send_lo, bytes, hipMemcpyDeviceToDevice, st));
+        // lo's last cz planes -> hi's lower halo
+        SD_HIP(hipMemcpyAsync(get(hi) + hh.recv_lo, get(lo) + hl.send_hi, bytes, hipMemcpyDeviceToDevice, st));
     }
     xbytes_ += int64_t(2) * (S - 1) * int64_t(bytes);
     xcopies_ += int64_t(2) * (S - 1);
     if (p_.nranks > 1) {
-        const size_t count = size_t(cz) * plane;
+        const size_t count = size_t(cz) * size_t(plane);
         SD_NCCL(ncclGroupStart());
         if (p_.rank > 0) {
             SlabState& s0 = slabs_[0];
-            SD_NCCL(ncclSend(get(s0), count, ncclFloat, p_.rank - 1, comm_, st));
-            SD_NCCL(ncclRecv(get(s0) + size_t(s0.g.Mz - cz) * plane, count, ncclFloat,
-                             p_.rank - 1, comm_, st));
+            const HaloPlan h = hp(s0);
+            SD_NCCL(ncclSend(get(s0) + h.send_lo, count, ncclFloat, p_.rank - 1, comm_, st));
+            SD_NCCL(ncclRecv(get(s0) + h.recv_lo, count, ncclFloat, p_.rank - 1, comm_, st));
         }
         if (p_.rank < p_.nranks - 1) {
             SlabState& sl = slabs_[S - 1];
-            SD_NCCL(ncclSend(get(sl) + size_t(sl.g.nz - cz) * plane, count, ncclFloat,
-                             p_.rank + 1, comm_, st));
-            SD_NCCL(ncclRecv(get(sl) + size_t(sl.g.nz) * plane, count, ncclFloat, p_.rank + 1,
-                             comm_, st));
+            const HaloPlan h = hp(sl);
+            SD_NCCL(ncclSend(get(sl) + h.send_hi, count, ncclFloat, p_.rank + 1, comm_, st));
+            SD_NCCL(ncclRecv(get(sl) + h.recv_hi, count, ncclFloat, p_.rank + 1, comm_, st));
         }
         SD_NCCL(ncclGroupEnd());
         const int nsend = (p_.rank > 0 ? 1 : 0) + (p_.rank < p_.nranks - 1 ? 1 : 0);
@@ -634,20 +647,24 @@ void Session::group_exchange_begin(int gi, bool which, HostBarrier& bar) {
         if (o >= 0 && o < G) SD_HIP(hipStreamWaitEvent(gr.xstream, groups_[o].ev_bnd, 0));
     if (gi == 0) tstart(5, gr.xstream);
     if (cz > 0) {
-        const size_t plane = plane_floats();
-        const size_t bytes = size_t(cz) * plane * sizeof(float);
+        const int64_t plane = int64_t(plane_floats());
+        const size_t bytes = size_t(cz) * size_t(plane) * sizeof(float);
         for (int s = gr.s0; s < gr.s1; ++s) {
             SlabState& me = slabs_[s];
-            if (s > 0) {  // lower neighbour's last cz planes -> my lower halo [Mz - cz, Mz)
+            const HaloPlan hm = halo_plan(me.g.nz, me.g.Mz, cz, plane);
+            if (s > 0) {  // lower neighbour's last cz planes -> my lower halo
                 SlabState& lo = slabs_[s - 1];
-                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + size_t(me.g.Mz - cz) * plane,
-                                      buf_ptr(lo, which, backend_) + size_t(lo.g.nz - cz) * plane, bytes,
-                                      hipMemcpyDefault, gr.xstream));
+                const HaloPlan hl = halo_plan(lo.g.nz, lo.g.Mz, cz, plane);
+                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + hm.recv_lo,
+                                      buf_ptr(lo, which, backend_) + hl.send_hi, bytes, hipMemcpyDefault,
+                                      gr.xstream));
             }
-            if (s < S - 1) {  // upper neighbour's first cz planes -> my upper halo [nz, nz + cz)
+            if (s < S - 1) {  // upper neighbour's first cz planes -> my upper halo
                 SlabState& hi = slabs_[s + 1];
-                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + size_t(me.g.nz) * plane,
-                                      buf_ptr(hi, which, backend_), bytes, hipMemcpyDefault, gr.xstream));
+                const HaloPlan hh = halo_plan(hi.g.nz, hi.g.Mz, cz, plane);
+                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + hm.recv_hi,
+                                      buf_ptr(hi, which, backend_) + hh.send_lo, bytes, hipMemcpyDefault,
+                                      gr.xstream));
             }
             const int npull = (s > 0 ? 1 : 0) + (s < S - 1 ? 1 : 0);
             xbytes_ += int64_t(npull) * int64_t(bytes);
@@ -711,9 +728,14 @@ void Session::run(int iters, double lambda, double* stats) {
         if (slabs_.size() > 1 || p_.nranks > 1) poisoned_ = true;
         throw;
     }
-    if (backend_ == 0 && !warned_fallback_) {
+    static const bool verbose = [] {
+        const char* e = std::getenv("SPIMDECON_VERBOSE");
+        return e && e[0] && e[0] != '0';
+    }();
+    if (backend_ == 0 && verbose && !warned_fallback_) {
         // the fast paths are a layout choice, not a semantic one: a slab outside them runs
         // the Stockham passes with the same results, several times slower -- say so once
+        // when asked (SPIMDECON_VERBOSE=1; callers can query mvd_xpass_mode / mvd_zpass_mode)
         for (int s = 0; s < int(slabs_.size()); ++s) {
             const int xm = slabs_[s].sp.xmode_update, zm = zpass_mode(s);
             if (xm != 2 || (zm != 2 && zm != 3)) {

@@ -74,6 +74,19 @@ struct DevGroup {
     DBuf<double> stats;                     // iters * V * {sum, max} of this group's slabs
 };
 
+// The halo transfers of one slab, as element offsets into its spectrum buffer (plane =
+// elements per padded z-plane).  The slab's interior planes are [0, nz); its upper halo
+// is [nz, nz + cz), its lower halo the wrapped planes [Mz - cz, Mz).
+//   to / from the LOWER neighbour: send [0, cz) (send_lo), receive into recv_lo
+//   to / from the UPPER neighbour: send [nz - cz, nz) (send_hi), receive into recv_hi
+// One helper for every deployment: the local copies between slabs of a device, the
+// device-group peer pulls and the RCCL send / recv all address the buffers through it,
+// so the one-GPU device-group tests exercise the offsets RCCL uses.
+struct HaloPlan {
+    int64_t send_lo, recv_lo, send_hi, recv_hi, count;
+};
+HaloPlan halo_plan(int64_t nz, int64_t Mz, int64_t cz, int64_t plane);
+
 // reusable host barrier for the group threads; abort() releases every waiter with an
 // error so that one failing thread cannot deadlock the others
 class HostBarrier {

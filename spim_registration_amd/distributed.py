@@ -41,6 +41,16 @@ def halo_planes_needed(z0: int, z1: int, nz: int, cz: int):
     return lower, upper
 
 
+def halo_plan(nz: int, Mz: int, cz: int, plane_elems: int):
+    """Float offsets of one slab's halo transfers (C-ABI ``mvd_halo_plan``, the helper
+    behind libspimdecon's local copies, device-group pulls and RCCL send / recv):
+    dict send_lo, recv_lo, send_hi, recv_hi, count."""
+    lib = _lib.load()
+    out = (C.c_int64 * 5)()
+    _lib.check(lib.mvd_halo_plan(int(nz), int(Mz), int(cz), int(plane_elems), out))
+    return dict(zip(("send_lo", "recv_lo", "send_hi", "recv_hi", "count"), list(out)))
+
+
 def unique_id_bytes() -> bytes:
     """128-byte RCCL unique id created on this process (rank 0)."""
     lib = _lib.load()

@@ -217,6 +217,10 @@ class InterestPointList:
         """loadInterestPoints (:178-220): False when the file cannot be read (the
         reference catches the IOException); a malformed line raises (Java's
         NumberFormatException is not caught there either)."""
+        # the reference starts a fresh list before opening the file (:184): a failed
+        # load leaves it empty, never the previous points (a malformed line raises, as
+        # the reference's NumberFormatException does; its partial list is not kept here)
+        self.interest_points = []
         lib = _lib.load()
         n = C.c_int64(0)
         st = lib.spim_load_interest_points(self.base_dir.encode(), self.file.encode(), None, None, 0, C.byref(n))
@@ -231,6 +235,12 @@ class InterestPointList:
         self.interest_points = [InterestPoint(int(ids[i]), (arr[i].pos[0], arr[i].pos[1], arr[i].pos[2]))
                                 for i in range(int(n.value))]
         return True
+
+
+def set_java_version(jdk: int) -> None:
+    """Double.toString form used by the .ip.txt writer: 8 (default, Fiji's Java 8
+    FloatingDecimal) or 19 (JDK 19+ shortest round trip)."""
+    check(_lib.load().spim_set_java_version(int(jdk)))
 
 
 def java_double_to_string(d: float) -> str:

@@ -155,3 +155,29 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     del imgs, ws
     lap("rl_result", t)
     return TimepointResult(psi, points, corr, psfs, stats, ms, engine)
+
+
+class Pipeline:
+    """The per-timepoint driver held across a time series (BASELINE configs[3]): the
+    parameters of every stage, and the device whose library-side state (the DoG
+    workspace, the PSF / resampling scratch, plan caches) carries over from one
+    timepoint to the next -- as the reference's plugin processes timepoint after
+    timepoint (EfficientBayesianBased.java:166-286).  Carried state must not change a
+    result: timepoint t processed after others equals timepoint t processed alone
+    (``result_digest``; tests/test_gpu_scale.py)."""
+
+    def __init__(self, **params):
+        self.params = params
+
+    def process(self, views, models, bb_min, bb_dims, log=None) -> TimepointResult:
+        return process_timepoint(views, models, bb_min, bb_dims, log=log, **self.params)
+
+
+def result_digest(res: TimepointResult) -> dict:
+    """SHA-256 of psi's bytes and of the RL statistics, plus the detection counts."""
+    import hashlib
+    psi = res.psi.cpu().numpy()
+    return {"psi_sha256": hashlib.sha256(psi.tobytes()).hexdigest(),
+            "stats_sha256": hashlib.sha256(np.ascontiguousarray(res.stats, np.float64).tobytes()).hexdigest(),
+            "points_sha256": hashlib.sha256(b"".join(np.ascontiguousarray(p, np.float64).tobytes()
+                                                     for p in res.points)).hexdigest()}

@@ -142,3 +142,76 @@ def test_slab_decomposition_gloo_world2():
     assert ok[1] < 1e-6, ok          # slab decomposition == whole volume
     assert ok[2] < 1e-6, ok          # all-reduced per-view statistics
     assert all(o[-1] for o in out)   # RCCL id broadcast delivered rank 0's bytes
+
+
+# ---------------------------------------------------------------------------- halo plan
+# The RCCL send / recv offsets, the device-group peer pulls and the local slab copies
+# all come from one helper (mvd_halo_plan / session.cpp halo_plan).  Here the plan is
+# replayed as RCCL would execute it -- rank r sends [send_hi] to r + 1, which receives
+# it at [recv_lo]; rank r sends [send_lo] to r - 1, which receives it at [recv_hi] --
+# over the internal geometry of the 8-rank decompositions of BASELINE configs[2] (C3,
+# 1024 y-rows -> 8 y-slabs of 128 + 2*12 halo rows: Mz = 152 != nz) and configs[4] (C5,
+# 2048 y-rows -> 256 + 24 = 280), plus a ragged split; every rank's halo planes must
+# then hold exactly its neighbours' global planes.  (The gloo test above validates the
+# decomposition arithmetic with its own numpy exchange; this one pins the addresses.)
+
+from spim_registration_amd.distributed import halo_plan  # noqa: E402
+
+
+def _hp_geometry(plane_rows, Mx):
+    """floats per padded plane of the engine spectrum: 2 * Hp * My, Hp = 16-padded Mx/2+1."""
+    Hp = -(-(Mx // 2 + 1) // 16) * 16
+    return 2 * Hp * plane_rows
+
+
+@pytest.mark.parametrize("name,nglob,nranks,cz,My,Mx", [
+    ("C3", 1024, 8, 12, 536, 1050),     # internal (x, z, y): planes = y rows, My = padded z
+    ("C5", 2048, 8, 12, 1050, 2100),
+    ("ragged", 1000, 3, 15, 96, 128),
+])
+def test_halo_plan_replayed_as_rccl(name, nglob, nranks, cz, My, Mx):
+    plane_real = _hp_geometry(My, Mx)
+    P = 3                                    # small plane for the replay; offsets scale by plane
+    ranks = []
+    for r in range(nranks):
+        z0, z1 = slab_range(nglob, nranks, r)
+        nz = z1 - z0
+        Mz = nz + 2 * cz                     # the direct z pass pads exactly
+        h = halo_plan(nz, Mz, cz, P)
+        hr = halo_plan(nz, Mz, cz, plane_real)
+        # offsets are plane multiples of the same plan at the real plane size
+        for k in h:
+            assert hr[k] == h[k] // P * plane_real, (k, h, hr)
+        assert h["send_lo"] == 0 and h["recv_hi"] == nz * P and h["recv_lo"] == (Mz - cz) * P
+        assert h["send_hi"] == (nz - cz) * P and h["count"] == cz * P
+        buf = np.full(Mz * P, -1.0)
+        buf[:nz * P] = np.repeat(np.arange(z0, z1, dtype=np.float64), P)   # interior = global plane ids
+        ranks.append(dict(z0=z0, z1=z1, nz=nz, Mz=Mz, h=h, buf=buf))
+    sent = [r["buf"].copy() for r in ranks]  # sends read the pre-exchange buffers
+    for r, st in enumerate(ranks):
+        h = st["h"]
+        if r > 0:        # from the lower neighbour: its send_hi -> my recv_lo
+            lo = ranks[r - 1]
+            assert lo["h"]["count"] == h["count"]
+            st["buf"][h["recv_lo"]:h["recv_lo"] + h["count"]] = \
+                sent[r - 1][lo["h"]["send_hi"]:lo["h"]["send_hi"] + lo["h"]["count"]]
+        if r < nranks - 1:   # from the upper neighbour: its send_lo -> my recv_hi
+            hi = ranks[r + 1]
+            st["buf"][h["recv_hi"]:h["recv_hi"] + h["count"]] = \
+                sent[r + 1][hi["h"]["send_lo"]:hi["h"]["send_lo"] + hi["h"]["count"]]
+    for r, st in enumerate(ranks):
+        planes = st["buf"].reshape(st["Mz"], P)[:, 0]
+        nz, Mz = st["nz"], st["Mz"]
+        np.testing.assert_array_equal(planes[:nz], np.arange(st["z0"], st["z1"]))   # interior untouched
+        if r < nranks - 1:
+            np.testing.assert_array_equal(planes[nz:nz + cz], np.arange(st["z1"], st["z1"] + cz))
+        if r > 0:
+            np.testing.assert_array_equal(planes[Mz - cz:], np.arange(st["z0"] - cz, st["z0"]))
+    # first, middle and last rank: which transfers exist
+    assert ranks[0]["z0"] == 0 and ranks[-1]["z1"] == nglob
+
+
+def test_halo_plan_rejects_bad_geometry():
+    from spim_registration_amd import _lib
+    with pytest.raises(_lib.SpimDeconError):
+        halo_plan(10, 20, 6, 4)      # Mz < nz + 2 cz

@@ -220,3 +220,48 @@ def test_dog_workspace_release_and_reuse(gpu):
     _lib.check(_lib.load().spim_dog_release_workspace(0))
     b = dog.compute(img, localization=1, keep_intensity=True)
     assert [(p.location, p.intensity) for p in a] == [(p.location, p.intensity) for p in b]
+
+
+@pytest.mark.parametrize("zchunk", [None, "128"])
+def test_dog_partial_last_z_chunk_after_full_ones(gpu, zchunk, monkeypatch):
+    """The split z stage's last chunk partial and not the first: 300 planes at the
+    default 256-plane chunks (256 + 44) and at 128 (128 + 128 + 44) -- the boundary a
+    round-3 experiment build read past.  Bit-identical DoG image and peak list."""
+    if zchunk:
+        monkeypatch.setenv("SPIMDECON_DOG_ZC_CHUNK", zchunk)
+    img = bead_stack(shape=(300, 40, 72), cid=25)
+    pts, d = dog.compute(img, sigma=1.8, threshold=0.002, find_min=True, find_max=True, return_dog=True,
+                         keep_intensity=True)
+    exp, dref = dog_ref.process_dog(img, 1.8, 0.002, find_min=True, find_max=True)
+    np.testing.assert_array_equal(d, dref)
+    assert len(exp) > 5
+    assert [tuple(int(c) for c in p.location) for p in pts] == [e[:3] for e in exp]
+    np.testing.assert_array_equal([p.intensity for p in pts], np.float32([e[3] for e in exp]))
+
+
+def test_dog_own_range_division_edges(gpu, monkeypatch):
+    """k_dog_xy skips the per-value range check of its reciprocal division when min / max
+    are the image's own (SPIMDECON_DOG_MM_EXACT=1, the default).  At the edges of that
+    argument -- min = -2^-20, values one ulp above min, a range near 2^48 -- the DoG
+    image and the ordered peaks must equal those of the checked division (=0), bit for
+    bit, and the oracle's."""
+    rng = np.random.default_rng(77)
+    img = bead_stack(shape=(40, 44, 48), cid=26)
+    mn = np.float32(-2.0 ** -20)
+    img[5, 5, 5] = mn
+    up = np.nextafter(mn, np.float32(1))
+    idx = rng.integers(0, img.size, 400)
+    img.reshape(-1)[idx] = up
+    img[30, 30, 30] = np.float32(2.0 ** 48)
+    img[31, 10, 7] = np.float32(2.0 ** 48) - np.float32(2.0 ** 24)
+    out = {}
+    for mm in ("1", "0"):
+        monkeypatch.setenv("SPIMDECON_DOG_MM_EXACT", mm)
+        pk, d = dog.compute(img, sigma=1.8, threshold=1e-9, find_min=True, find_max=True, return_dog=True,
+                            keep_intensity=True)
+        out[mm] = ([(p.location, p.intensity) for p in pk], d)
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    assert out["1"][0] == out["0"][0]
+    exp, dref = dog_ref.process_dog(img, 1.8, 1e-9, find_min=True, find_max=True)
+    np.testing.assert_array_equal(out["1"][1], dref)
+    assert [tuple(int(c) for c in q[0]) for q in out["1"][0]] == [e[:3] for e in exp]

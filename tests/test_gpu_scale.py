@@ -9,11 +9,13 @@
                2 iterations, finite, exact final mask, sumChange falling
   C5 rank slab the geometry one of 8 ranks holds (2048x256x1024 + halos, padded
                2100x1050x280) through the y-split path vs the rocFFT backend, 1e-5
-  C5 aspect    the same decomposition on a 256x256x128 instance vs the oracle, 1e-4
+  C5 aspect    the same decomposition on a 232x256x104 instance vs the oracle, 1e-4, on
+               C5's fp16 two-factor x tiles (asserted)
   C4           one timepoint of 8-view 768^3 through pipeline.process_timepoint:
                input preparation vs the oracle on sub-boxes, PSFs vs the oracle per view,
                10 RL iterations (800-point lengths, 31-plane kernels) vs the rocFFT
-               backend on the same prepared inputs and PSFs
+               backend on the same prepared inputs and PSFs; two timepoints back to back
+               through one Pipeline == a fresh process's timepoint, bit for bit
 
 References (paths under /root/reference/src/main/java/spim/process/):
 fusion/deconvolution/MVDeconvolution.java:333-444 (the iteration),
@@ -169,23 +171,26 @@ def test_c5_rank_slab_geometry_vs_rocfft(gpu):
 
 
 @pytest.mark.timeout(300)
-def test_c5_decomposition_matches_oracle_256x256x128(gpu):
+def test_c5_decomposition_matches_oracle_232x256x104(gpu):
     """C5's decomposition (8 y-slabs, fp16 img / weight storage, OPTIMIZATION_I 0.006)
-    on an instance the oracle runs in seconds; the oracle sees the fp16-rounded inputs."""
-    imgs, ws, ks, _ = synthetic.make_views((128, 256, 256), 6, config_id=52, ksize=(25, 25, 25),
+    on an instance the oracle runs in seconds, on C5's own arithmetic path: x = 232 + 24
+    pads to 256, a two-factor tile length, so every slab runs the fp16 x tiles
+    (k_xtile<..., S = 1, ...>) -- asserted -- and the direct z pass.  The oracle sees the
+    fp16-rounded inputs (MVDeconvolution.java:582-703 on the stored values)."""
+    imgs, ws, ks, _ = synthetic.make_views((104, 256, 232), 6, config_id=52, ksize=(25, 25, 25),
                                            weights="blend", partial=True)
-    with Session((256, 256, 128), storage_fp16=True, local_slabs=8) as s:
+    with Session((232, 256, 104), storage_fp16=True, local_slabs=8) as s:
         for i, w, k in zip(imgs, ws, ks):
             s.add_view(i, w, k)
         s.init(PSFTYPE.OPTIMIZATION_I)
         s.init_psi()
         st = s.run(2, 0.006)
         s.apply_mask()
-        assert s.num_slabs() == 8 and s.slab_extent(0) == (256, 128, 32)
-        # x = 256 + 24 = 280 is not a two-factor tile length (C5's 2100 is: the two tests
-        # above assert xpass 2 at the real geometry); the z pass is the direct one
+        # y-slabs of 32 rows, kept as (x, z, y) rows: padded 256 x 128 x 56
+        assert s.num_slabs() == 8 and s.slab_extent(0) == (232, 104, 32)
+        assert s.fft_dims(0)[0] == 256, s.fft_dims(0)
         xm, zm = engine_modes(s)
-        assert set(xm) <= {1, 2} and set(zm) <= {2, 3}, (xm, zm)
+        assert set(xm) == {2} and set(zm) <= {2, 3}, (xm, zm)
         psi = s.get_psi()
     hi = [i.astype(np.float16).astype(np.float32) for i in imgs]
     hw = [w.astype(np.float16).astype(np.float32) for w in ws]
@@ -251,3 +256,33 @@ def test_c4_timepoint_8view_768(gpu):
     err = rel_l2(psi, psir)
     log(f"RL engine vs rocFFT backend: rel-L2 {err:.2e}")
     assert err < ENGINE_VS_ROCFFT
+
+
+@pytest.mark.timeout(1200)
+def test_c4_two_timepoints_back_to_back_equal_fresh_process(gpu):
+    """Two C4 timepoints (8-view 768^3) back to back through one Pipeline (the DoG
+    workspace, PSF / resampling scratch and plan caches carried over): timepoint 1's psi,
+    RL statistics and detections equal, bit for bit, those of a fresh process that runs
+    timepoint 1 alone (tools/c4_pipeline.py --only 1 --digest)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    n = 768
+    pipe = pipeline.Pipeline(psf_size=(19, 19, 25), iterations=10)
+    digests = []
+    for t in (0, 1):
+        views, models = synthetic.make_timepoint_torch((n, n, n), (n, n, n), 8, timepoint=t, device="cuda:0")
+        res = pipe.process(views, models, (0, 0, 0), (n, n, n))
+        digests.append(pipeline.result_digest(res))
+        print(f"  [c4x2] timepoint {t}: {res.ms}", flush=True)
+        del views, res
+        release()
+    assert digests[0]["psi_sha256"] != digests[1]["psi_sha256"]     # the beads drift: a different result
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "c4_pipeline.py"), "--only", "1", "--digest",
+                        "--timepoints", "2"], capture_output=True, text=True, timeout=900, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    fresh = json.loads(r.stdout.strip().splitlines()[-1])["timepoints"][0]
+    for k in ("psi_sha256", "stats_sha256", "points_sha256"):
+        assert fresh[k] == digests[1][k], (k, fresh, digests[1])

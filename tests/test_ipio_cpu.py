@@ -9,9 +9,9 @@ import pytest
 
 from oracle import ip_ref
 from spim_registration_amd import _lib
-from spim_registration_amd.dog import InterestPoint, InterestPointList, java_double_to_string
+from spim_registration_amd.dog import InterestPoint, InterestPointList, java_double_to_string, set_java_version
 
-KNOWN = [  # java.lang.Double.toString (spec examples and boundaries)
+KNOWN = [  # java.lang.Double.toString, JDK 19+ (spec examples and boundaries)
     (1.0, "1.0"), (12.0, "12.0"), (100.0, "100.0"), (0.001, "0.001"), (0.0015, "0.0015"), (1e-4, "1.0E-4"),
     (9999999.0, "9999999.0"), (1e7, "1.0E7"), (1.5e7, "1.5E7"), (123.456, "123.456"), (-2.5, "-2.5"),
     (0.1 + 0.2, "0.30000000000000004"), (1e23, "1.0E23"), (0.0, "0.0"), (-0.0, "-0.0"),
@@ -20,33 +20,80 @@ KNOWN = [  # java.lang.Double.toString (spec examples and boundaries)
 ]
 
 
-def test_java_double_to_string_known_answers(lib):
+# JDK 8 (sun.misc.FloatingDecimal): the same strings as above except where its symmetric
+# half-ulp stopping test keeps going -- the anomalies documented for JDK <= 18
+# (JDK-4511638) -- plus the boundaries of its int / long / big-integer branches
+KNOWN8 = [(v, s) for v, s in KNOWN if v not in (1e23,)] + [
+    (2e23, "1.9999999999999998E23"), (8.41e21, "8.409999999999999E21"),
+    (2.82879384806159e17, "2.82879384806159008E17"), (1e23, "9.999999999999999E22"),
+    (2.0 ** 60, "1.15292150460684698E18"), (0.002, "0.002"), (1e-5, "1.0E-5"), (4.35, "4.35"),
+    (9007199254740992.0, "9.007199254740992E15"), (2.0 ** 63, "9.223372036854776E18"),
+]
+
+
+@pytest.fixture
+def jdk():
+    """Select a Java version for a test, restoring the default (8) afterwards."""
+    yield set_java_version
+    set_java_version(8)
+
+
+def test_java_double_to_string_known_answers(lib, jdk):
+    jdk(19)
     for v, s in KNOWN:
         assert ip_ref.java_double_to_string(v) == s, (v, s)
         assert java_double_to_string(v) == s, (v, s)
 
 
-def test_java_double_to_string_matches_oracle_random(lib):
-    rng = np.random.default_rng(5)
-    vals = np.concatenate([rng.random(2000) * 2048, rng.normal(0, 1, 500), 10.0 ** rng.uniform(-8, 12, 500),
+def test_java8_double_to_string_known_answers(lib, jdk):
+    jdk(8)
+    for v, s in KNOWN8:
+        assert ip_ref.java8_double_to_string(v) == s, (v, s)
+        assert java_double_to_string(v) == s, (v, s)
+
+
+def _random_doubles(seed, n_bits=4000):
+    rng = np.random.default_rng(seed)
+    bits = rng.integers(0, 2 ** 63, n_bits, dtype=np.uint64) | (rng.integers(0, 2, n_bits, dtype=np.uint64) << np.uint64(63))
+    raw = bits.view(np.float64)
+    return np.concatenate([rng.random(2000) * 2048, rng.normal(0, 1, 500), 10.0 ** rng.uniform(-8, 25, 1500),
                            rng.integers(0, 2048, 300).astype(np.float64),
-                           rng.random(300).astype(np.float32).astype(np.float64) * 1000])
-    for v in vals:
-        assert java_double_to_string(v) == ip_ref.java_double_to_string(v), v
-        assert float(java_double_to_string(v).replace("E", "e")) == v
+                           rng.random(300).astype(np.float32).astype(np.float64) * 1000, raw[np.isfinite(raw)]])
 
 
-def test_save_and_load_interest_points(lib, tmp_path):
+@pytest.mark.parametrize("version", [8, 19])
+def test_java_double_to_string_matches_oracle_random(lib, jdk, version):
+    jdk(version)
+    ref = ip_ref.java8_double_to_string if version == 8 else ip_ref.java_double_to_string
+    longer = 0
+    for v in _random_doubles(5 + version):
+        got = java_double_to_string(v)
+        assert got == ref(v), (v, version)
+        assert float(got.replace("E", "e")) == v                     # both forms round-trip
+        longer += got != ip_ref.java_double_to_string(v)
+    if version == 8:   # the JDK 8 form differs from the shortest one somewhere, never in value
+        assert longer > 0
+
+
+def test_java_version_must_be_8_or_19(lib):
+    with pytest.raises(_lib.SpimDeconError):
+        set_java_version(11)
+
+
+@pytest.mark.parametrize("version", [8, 19])
+def test_save_and_load_interest_points(lib, tmp_path, jdk, version):
+    jdk(version)
     rng = np.random.default_rng(6)
     pos = rng.random((257, 3)) * 700
     pos[:40] = np.floor(pos[:40])                         # localization 0: integer positions
+    pos[40] = (2e23, 8.41e21, 2.82879384806159e17)        # JDK 8 prints these long
     pts = [InterestPoint(i, tuple(p)) for i, p in enumerate(pos)]
     ipl = InterestPointList(tmp_path, "interestpoints/tpId_0_viewSetupId_3.beads")
     assert not ipl.save_interest_points()                  # no list yet (:68-71)
     ipl.set_interest_points(pts)
     assert ipl.save_interest_points()
     path = tmp_path / "interestpoints" / "tpId_0_viewSetupId_3.beads.ip.txt"
-    assert path.read_text() == ip_ref.ip_txt(pos)          # byte for byte
+    assert path.read_text() == ip_ref.ip_txt(pos, jdk=version)   # byte for byte
     back = InterestPointList(tmp_path, "interestpoints/tpId_0_viewSetupId_3.beads")
     assert back.load_interest_points()
     got = back.get_interest_points()
@@ -59,8 +106,12 @@ def test_load_skips_preamble_and_keeps_ids(lib, tmp_path):
     ipl = InterestPointList(str(tmp_path), "x")
     assert ipl.load_interest_points()
     assert [(p.id, p.location) for p in ipl.get_interest_points()] == [(7, (1.0, 2.5, 3e-4)), (9, (4.0, 5.0, 6.0))]
-    # a missing file is the reference's caught IOException: false, no exception (:209-214)
-    assert InterestPointList(str(tmp_path), "missing").load_interest_points() is False
+    # a missing file is the reference's caught IOException: false, no exception (:209-214),
+    # and the list is the fresh empty one the reference creates before opening (:184)
+    assert ipl.load_interest_points() and len(ipl.get_interest_points()) == 2
+    ipl.file = "missing"
+    assert ipl.load_interest_points() is False
+    assert ipl.get_interest_points() == []
 
 
 def test_load_trims_fields_like_java(lib, tmp_path):
@@ -73,6 +124,36 @@ def test_load_trims_fields_like_java(lib, tmp_path):
     (tmp_path / "bad.ip.txt").write_text("id\tx\ty\tz\n3\tabc\t2.0\t4.0\n")
     with pytest.raises(_lib.SpimDeconError):
         InterestPointList(str(tmp_path), "bad").load_interest_points()
+
+
+@pytest.mark.parametrize("line", [
+    "3\t\t1.5\t2\t4",          # an empty field: parseDouble("") throws (not shifted over)
+    "3\t1.5\t2",                # fewer than 4 fields: p[3] is out of bounds
+    "",                          # an empty line: "".split("\t") = [""]
+    "3\tinf\t2\t4",             # strtod would take these; parseDouble does not
+    "3\tnan\t2\t4",
+    "3\t1.5\t2\t 4 x",
+    "3.0\t1.5\t2\t4",           # parseInt rejects a decimal id
+    "3\t1.5e\t2\t4",
+    "3\t..5\t2\t4",
+])
+def test_load_rejects_what_java_rejects(lib, tmp_path, line):
+    (tmp_path / "r.ip.txt").write_text("id\tx\ty\tz\n" + line + "\n")
+    with pytest.raises(_lib.SpimDeconError):
+        InterestPointList(str(tmp_path), "r").load_interest_points()
+
+
+def test_load_accepts_what_java_accepts(lib, tmp_path):
+    """Double.parseDouble forms: signs, Infinity / NaN, exponents, a d/f suffix, hex floats;
+    extra fields past the fourth are ignored, trailing tabs dropped by split."""
+    (tmp_path / "a.ip.txt").write_text("id\tx\ty\tz\n-3\t+1.5\t-Infinity\tNaN\n4\t1e2\t.5\t7.d\textra\n"
+                                       "5\t0x1.8p1\t2f\t1E-3\t\t\n")
+    ipl = InterestPointList(str(tmp_path), "a")
+    assert ipl.load_interest_points()
+    got = [(p.id, p.location) for p in ipl.get_interest_points()]
+    assert got[0][0] == -3 and got[0][1][:2] == (1.5, float("-inf")) and math.isnan(got[0][1][2])
+    assert got[1] == (4, (100.0, 0.5, 7.0))
+    assert got[2] == (5, (3.0, 2.0, 0.001))
 
 
 def test_convolution_cpu_has_no_cpu_path(lib):

@@ -70,11 +70,46 @@ __global__ __launch_bounds__(512) void k_pattern(float4* buf, long E, int P, int
     }
 }
 
-__global__ __launch_bounds__(512) void k_stream(float4* buf, long n) {
-    for (long i = blockIdx.x * 512L + threadIdx.x; i < n; i += long(gridDim.x) * 512) {
-        float4 w = buf[i];
-        w.x += 1.0f;
-        buf[i] = w;
+// Contiguous references.  Round 3's k_stream kept ONE dependent float4 load -> store
+// per thread in flight (4.7-4.9 TB/s); these keep DEPTH independent float4 loads per
+// thread in flight before their stores (a block's DEPTH * 512 * 16 B = one chunk).
+// k_rmw: in place (the z pass's shape); k_copy: read src, write dst (the guide's copy).
+template <int DEPTH>
+__global__ __launch_bounds__(256) void k_rmw(float4* buf, long n) {
+    const long chunk = long(DEPTH) * 256;
+    for (long base = long(blockIdx.x) * chunk; base < n; base += long(gridDim.x) * chunk) {
+        float4 v[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long i = base + d * 256 + threadIdx.x;
+            if (i < n) v[d] = buf[i];
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long i = base + d * 256 + threadIdx.x;
+            if (i < n) {
+                v[d].x += 1.0f;
+                buf[i] = v[d];
+            }
+        }
+    }
+}
+
+template <int DEPTH>
+__global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, long n) {
+    const long chunk = long(DEPTH) * 256;
+    for (long base = long(blockIdx.x) * chunk; base < n; base += long(gridDim.x) * chunk) {
+        float4 v[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long i = base + d * 256 + threadIdx.x;
+            if (i < n) v[d] = src[i];
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long i = base + d * 256 + threadIdx.x;
+            if (i < n) dst[i] = v[d];
+        }
     }
 }
 
@@ -120,18 +155,56 @@ int main() {
         std::printf("%d %d %d %d %d %.4f %.3f\n", v.seg * 8, v.zb, v.stag, v.grid, v.depth, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
         std::fflush(stdout);
     }
-    for (int grid : {1024, 4096}) {   // contiguous reference
-        hipLaunchKernelGGL(k_stream, dim3(grid), dim3(512), 0, 0, buf, long(bytes / 16));
-        CK(hipDeviceSynchronize());
-        CK(hipEventRecord(a));
-        for (int r = 0; r < 10; ++r) hipLaunchKernelGGL(k_stream, dim3(grid), dim3(512), 0, 0, buf, long(bytes / 16));
-        CK(hipEventRecord(b));
-        CK(hipEventSynchronize(b));
-        float ms;
-        CK(hipEventElapsedTime(&ms, a, b));
-        ms /= 10;
-        std::printf("contiguous grid %d %.4f ms %.3f TB/s\n", grid, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
-    }
+    // plane-strided pattern at higher occupancy (grid 2048-4096 blocks of 8 waves)
+    for (int seg : {32, 64})
+        for (int grid : {2048, 4096}) {
+            auto launch = [&] { hipLaunchKernelGGL(k_pattern<8>, dim3(grid), dim3(512), 0, 0, buf, E, P, seg, 1, 1); };
+            launch();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(a));
+            for (int r = 0; r < 10; ++r) launch();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            ms /= 10;
+            std::printf("%d 1 1 %d 8 %.4f %.3f\n", seg * 8, grid, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
+            std::fflush(stdout);
+        }
+    // contiguous references: in place (read + write the same bytes) and copy (src -> dst)
+    float4* dst;
+    CK(hipMalloc(&dst, bytes));
+    CK(hipMemset(dst, 0, bytes));
+    const long n = long(bytes / 16);
+    std::printf("kind depth grid(256-thread blocks) ms TB/s(read+write)\n");
+    for (int kind = 0; kind < 2; ++kind)
+        for (int depth : {1, 4, 8})
+            for (int grid : {2048, 8192, 32768}) {
+                auto launch = [&] {
+                    if (kind == 0) {
+                        if (depth == 1) hipLaunchKernelGGL(k_rmw<1>, dim3(grid), dim3(256), 0, 0, buf, n);
+                        else if (depth == 4) hipLaunchKernelGGL(k_rmw<4>, dim3(grid), dim3(256), 0, 0, buf, n);
+                        else hipLaunchKernelGGL(k_rmw<8>, dim3(grid), dim3(256), 0, 0, buf, n);
+                    } else {
+                        if (depth == 1) hipLaunchKernelGGL(k_copy<1>, dim3(grid), dim3(256), 0, 0, buf, dst, n);
+                        else if (depth == 4) hipLaunchKernelGGL(k_copy<4>, dim3(grid), dim3(256), 0, 0, buf, dst, n);
+                        else hipLaunchKernelGGL(k_copy<8>, dim3(grid), dim3(256), 0, 0, buf, dst, n);
+                    }
+                };
+                launch();
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(a));
+                for (int r = 0; r < 10; ++r) launch();
+                CK(hipEventRecord(b));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                ms /= 10;
+                std::printf("%s %d %d %.4f %.3f\n", kind == 0 ? "rmw" : "copy", depth, grid, ms,
+                            2.0 * bytes / (ms * 1e-3) / 1e12);
+                std::fflush(stdout);
+            }
+    CK(hipFree(dst));
     CK(hipFree(buf));
     return 0;
 }
