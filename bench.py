@@ -107,6 +107,7 @@ def plan_gpus(args, env, visible):
 
 # engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
 PMC_KERNELS = {"z_convolve": ("k_zdmc<", "k_zdma<", "k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
+               "yzy": ("k_yzy<",),
                "x_update": ("k_xtile<2,", "k_xrows<2,", "k_xpass<2,"),
                "x_quotient": ("k_xtile<1,", "k_xrows<1,", "k_xpass<1,")}
 
@@ -192,6 +193,16 @@ def engine_classes(geom, wb):
     zw = 8.0 * nzi / Mz
     zb = 8.0 + zw + kz
     yb = 8.0 * (1.0 + nzi / Mz)
+    if geom.get("yzy"):
+        # fused y-z-y pass (z pass mode 4): reads the Mz x-spectrum planes, writes the nz
+        # result planes to the other buffer, reads the kernel: the z pass's bytes, once
+        classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
+                   ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
+                   ("stats_reduce", 0, 0, 0), ("yzy", 0, 0, zb)]
+        b_view = (12 + 2 * wb) * N + (32.0 + 2 * zb) * S
+        model = (f"V*((12+2w)N + (32+2c)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
+                 f"c = fused y-z-y bytes per bin = {zb:.3f} (8 read + {zw:.3f} write + {kz:.3f} kernel)")
+        return classes, b_view, model
     classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
                ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
                ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 16 + kz)]
@@ -266,7 +277,8 @@ def slab_geom(sess, nslabs, ngpus):
     M = sess.fft_dims(0)
     ext = sess.slab_extent(0)              # internal (x, y, z) voxels of slab 0
     return {"M": M, "N": ext[0] * ext[1] * ext[2], "S": (M[0] // 2 + 1) * M[1] * M[2],
-            "nz_int": ext[2], "Mz": M[2], "kplanes": sess.kernel_planes(0), "nslabs": nslabs, "ngpus": ngpus}
+            "nz_int": ext[2], "Mz": M[2], "kplanes": sess.kernel_planes(0), "nslabs": nslabs, "ngpus": ngpus,
+            "yzy": sess.zpass_mode(0) == 4}
 
 
 def main(argv=None):
@@ -364,7 +376,7 @@ def main(argv=None):
         return max_over_ranks(t)
 
     def placement(s):
-        """devices, slabs and the engine pass each slab ran (fast: x pass 2, z pass 2/3);
+        """devices, slabs and the engine pass each slab ran (fast: x pass 2, z pass 2/3/4);
         a run outside the fast passes is refused unless --allow-fallback."""
         ns = s.num_slabs()
         out = {"num_devices": s.num_devices(), "slabs": ns,
@@ -372,7 +384,7 @@ def main(argv=None):
         if args.backend == "engine":
             out["xpass_modes"] = sorted({s.xpass_mode(i) for i in range(ns)})
             out["zpass_modes"] = sorted({s.zpass_mode(i) for i in range(ns)})
-            fast = out["xpass_modes"] == [2] and set(out["zpass_modes"]) <= {2, 3}
+            fast = out["xpass_modes"] == [2] and set(out["zpass_modes"]) <= {2, 3, 4}
             if not fast and not args.allow_fallback:
                 raise SystemExit(f"engine fallback (x pass {out['xpass_modes']}, z pass {out['zpass_modes']}): "
                                  "refusing to report it; --allow-fallback to measure anyway")

@@ -265,7 +265,9 @@ int mvd_kernel_planes(mvd_session* h, int slab, int* planes);
 /* z pass of the engine (info/bench): 0 = fused FFT z pass with full kernel
  * spectra, 1 = fused FFT z pass with compact kernels, 2 = direct circular
  * convolution with the compact kernel (only the nz interior planes written),
- * 3 = the same over z chunks carried inside a block; -1 for the rocFFT backend */
+ * 3 = the same over z chunks carried inside a block, 4 = the fused y-z-y pass (y
+ * transforms and the direct z convolution in one pass over kx-major spectra);
+ * -1 for the rocFFT backend */
 int mvd_zpass_mode(mvd_session* h, int slab, int* mode);
 /* x pass of the last update launch of slab s (info/tests): 2 = two-factor row-pair
  * tiles, 1 = per-wave rows, 0 = Stockham rows, -1 = no run yet, -2 = rocFFT backend */

@@ -434,6 +434,7 @@ constexpr int kCThreads = 1024;
 #include "fftconv_x.inc"
 #include "fftconv_xt.inc"
 #include "fftconv_zd.inc"
+#include "fftconv_yzy.inc"
 
 // ------------------------------------------------------------------ host side
 
@@ -549,6 +550,25 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
+    if (p.kxl) {   // kx-major spectra (the fused y-z-y pass): 8 row pairs per tile only
+#define SD_XK(SV, A, B, TK)                                                                                     \
+        if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                                 \
+            constexpr int TRv = SD_2F_TR(A, B);                                                                 \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, 8, TRv, true>), \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(xt_lds(L, 8, xt_twg(L, 8))))); \
+            hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, 8, TRv, true>), dim3(ntiles8), dim3(8 * TRv),             \
+                               xt_lds(L, 8, xt_twg(L, 8)), s, b);                                                   \
+            done = true;                                                                                        \
+        }
+        const int64_t ntiles8 = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(8)));
+#define SD_XK_S(A, B) SD_XK(0, A, B, false) SD_XK(1, A, B, false) if constexpr (MODE == XM_UPDATE) { SD_XK(0, A, B, true) SD_XK(1, A, B, true) }
+        SD_X2F_SIZES(SD_XK_S)
+#undef SD_XK_S
+#undef SD_XK
+        SD_CHECK(done, SPIMDECON_ERR_ARG, "no kx-major x tile for this length");
+        SD_HIP(hipGetLastError());
+        return unsigned(ntiles8);
+    }
 #define SD_XT(SV, A, B, TK, NP)                                                                            \
     if (!done && np == NP && sv == SV && L == (A) * (B) && tik == TK) {                                   \
         constexpr int TRv = SD_2F_TR(A, B);                                                               \
@@ -624,6 +644,7 @@ unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s
             return gt;
         }
     }
+    SD_CHECK(!p.kxl, SPIMDECON_ERR_STATE, "kx-major spectra need the x tiles (engine_yzy_ok)");
     if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
         if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) {
             if (MODE == XM_UPDATE) p.xmode_update = 1;
@@ -1146,6 +1167,82 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
     }
     const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz, int(p.g.nz));
     SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
+}
+
+// ---------------------------------------------------------------- fused y-z-y pass
+#define SD_YZY_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24)
+constexpr int kYzyG = 8;
+
+static bool yzy_enabled() {
+    const char* e = std::getenv("SPIMDECON_YZY");   // read per session (tests toggle it)
+    return !(e && e[0] == '0');
+}
+
+bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox) {
+    const int L = int(p.g.My);
+    const int KC = p.g.cz;
+    if (!yzy_enabled() || !kcompact || !zexact || p.g.Mz != p.g.nz + 2 * KC) return false;
+    if (KC != 4 && KC != 8 && KC != 12) return false;
+    bool ylen = false;
+#define SD_YL(A, B) ylen = ylen || (p.fy.n1 == (A) && p.fy.n2 == (B));
+    SD_YZY_SIZES(SD_YL)
+#undef SD_YL
+    if (!ylen || L % 2 != 0 || yzy_lds(L, KC, kYzyG) > 160 * 1024) return false;
+    // the kx-major x tiles: a two-factor x length, 16-B voxel rows, 32-bit buffer ranges
+    bool xlen = false;
+#define SD_XL(A, B) xlen = xlen || p.g.Mx == (A) * (B);
+    SD_X2F_SIZES(SD_XL)
+#undef SD_XL
+    const int Lx = int(p.g.Mx);
+    return xlen && p.fx.n1 && xt_lds(Lx, 8, xt_twg(Lx, 8)) <= 160 * 1024 && p.g.nx % 4 == 0 &&
+           uint64_t(p.spectrum_elems()) * sizeof(float2) < kOOB && uint64_t(nvox) * 4u < kOOB;
+}
+
+void engine_kernel_kxmajor(const SpectralPlan& p, const float2* Kc, float2* Kt, hipStream_t s) {
+    const int NQ = 2 * p.g.cz + 1;
+    const dim3 grid(unsigned(ceil_div(p.Hx, int64_t(32))), unsigned(ceil_div(p.g.My, int64_t(32))), unsigned(NQ));
+    hipLaunchKernelGGL(k_kernel_kxmajor, grid, dim3(256), 0, s, Kc, Kt, NQ, int(p.g.My), p.Hp, int(p.Hx));
+    SD_HIP(hipGetLastError());
+}
+
+int64_t engine_kernel_kxmajor_elems(const SpectralPlan& p) { return int64_t(2 * p.g.cz + 1) * p.g.My * p.Hx; }
+
+void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const float2* Kt, hipStream_t s) {
+    SD_CHECK(p.kxl, SPIMDECON_ERR_STATE, "the fused y-z-y pass needs kx-major spectra");
+    YzyArgs a;
+    a.Cin = Cin;
+    a.Cout = Cout;
+    a.Kt = Kt;
+    a.tw = p.fy.tw;
+    a.Hp = p.Hp;
+    a.Hx = int(p.Hx);
+    a.My = int(p.g.My);
+    a.Mz = int(p.g.Mz);
+    a.nz = int(p.g.nz);
+    a.nch = int(ceil_div(p.g.nz, int64_t(kYzyG)));
+    a.kscale = float(p.g.Mz);
+    static const int grid_env = [] {   // SPIMDECON_YZY_GRID: blocks (A/B runs; default one per CU)
+        const char* e = std::getenv("SPIMDECON_YZY_GRID");
+        return e ? std::max(1, std::atoi(e)) : 256;
+    }();
+    const unsigned grid = unsigned(std::min<int64_t>(grid_env, int64_t(a.Hx) * a.nch));
+    const int KC = p.g.cz;
+    bool done = false;
+#define SD_YZ1(A, B, KCV)                                                                                  \
+    if (!done && p.fy.n1 == (A) && p.fy.n2 == (B) && KC == (KCV)) {                                        \
+        constexpr int Tv = ((A) * (B) + 63) / 64 * 64;                                                     \
+        const size_t lds = yzy_lds((A) * (B), KCV, kYzyG);                                                 \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, kYzyG, Tv>),             \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
+        hipLaunchKernelGGL((k_yzy<A, B, KCV, kYzyG, Tv>), dim3(grid), dim3(Tv), lds, s, a);                 \
+        done = true;                                                                                       \
+    }
+#define SD_YZ(A, B) SD_YZ1(A, B, 4) SD_YZ1(A, B, 8) SD_YZ1(A, B, 12)
+    SD_YZY_SIZES(SD_YZ)
+#undef SD_YZ
+#undef SD_YZ1
+    SD_CHECK(done, SPIMDECON_ERR_ARG, "no fused y-z-y kernel for this geometry");
+    SD_HIP(hipGetLastError());
 }
 
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {

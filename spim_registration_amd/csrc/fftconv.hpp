@@ -50,6 +50,8 @@ struct SpectralPlan {
     // x pass the last update launch ran: 2 = two-factor tiles (k_xtile), 1 = per-wave
     // rows (k_xrows), 0 = Stockham rows (k_xpass); -1 = none yet (mvd_xpass_mode)
     mutable int xmode_update = -1;
+    // kx-major spectra C[z][kx][y] (the fused y-z-y pass, engine_yzy); else C[z][y][kx]
+    bool kxl = false;
     int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
     // allow_2f: use the two-factor register kernels for lengths in the fast-path table
     // z_fft = false: no z transform plan (the direct z convolution needs none, and then
@@ -91,6 +93,16 @@ int64_t engine_kernel_compact_elems(const SpectralPlan& p);
 void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz, float scale,
                            float2* work, float2* Kc, hipStream_t s);
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s);
+// Fused y-z-y pass (fftconv_yzy.inc): Cout = y-inverse(z-convolve(y-forward(Cin), Kt))
+// over kx-major spectra (p.kxl), interior planes only; Cin keeps its contents.  It
+// applies when the slab runs the direct z pass with compact kernels, the y length is
+// a two-factor length up to 576 with its ring in the LDS, cz is 4, 8 or 12, and the x
+// length has kx-major x tiles (SPIMDECON_YZY=0 turns it off).
+bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox);
+// compact kernel [2cz+1][My][Hp] -> kx-major [Hx][2cz+1][My]
+int64_t engine_kernel_kxmajor_elems(const SpectralPlan& p);
+void engine_kernel_kxmajor(const SpectralPlan& p, const float2* Kc, float2* Kt, hipStream_t s);
+void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const float2* Kt, hipStream_t s);
 // Y pass: in-place complex FFT along y (inverse when inv)
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 // Forward y pass of the z planes [z0, z1) only (false: not available for this plan,

@@ -458,8 +458,28 @@ void Session::build_spectra() {
                     (which == 0 ? sl.e1spec : sl.e2spec).push_back(std::move(spec));
                 }
             }
+            // the fused y-z-y pass: kx-major spectra and kernels (the compact kernels are
+            // replaced by their kx-major transposes; no other pass reads them then)
+            sl.sp.kxl = engine_yzy_ok(sl.sp, sl.kcompact, sl.zexact, sl.n);
+            if (sl.sp.kxl) {
+                for (auto* ks : {&sl.e1spec, &sl.e2spec})
+                    for (auto& k : *ks) {
+                        DBuf<float2> kt(size_t(engine_kernel_kxmajor_elems(sl.sp)));
+                        engine_kernel_kxmajor(sl.sp, k.p, kt.p, stream_);
+                        SD_HIP(hipStreamSynchronize(stream_));
+                        k = std::move(kt);
+                    }
+            }
         }
         SD_HIP(hipStreamSynchronize(stream_));
+    }
+    if (backend_ == 0) {   // one layout for every slab (the exchanges copy whole planes)
+        bool any = false, all = true;
+        for (auto& sl : slabs_) {
+            any = any || sl.sp.kxl;
+            all = all && sl.sp.kxl;
+        }
+        SD_CHECK(any == all, SPIMDECON_ERR_STATE, "slabs disagree on the fused y-z-y pass");
     }
     spectra_ready_ = true;
 }
@@ -738,10 +758,10 @@ void Session::run(int iters, double lambda, double* stats) {
         // when asked (SPIMDECON_VERBOSE=1; callers can query mvd_xpass_mode / mvd_zpass_mode)
         for (int s = 0; s < int(slabs_.size()); ++s) {
             const int xm = slabs_[s].sp.xmode_update, zm = zpass_mode(s);
-            if (xm != 2 || (zm != 2 && zm != 3)) {
+            if (xm != 2 || (zm != 2 && zm != 3 && zm != 4)) {
                 std::fprintf(stderr,
                              "[spimdecon] warning: slab %d (%lld x %lld x %lld, padded %lld x %lld x %lld) runs "
-                             "outside the fast engine passes (x pass %d, z pass %d; fast = 2 and 2/3): same "
+                             "outside the fast engine passes (x pass %d, z pass %d; fast = 2 and 2/3/4): same "
                              "results, lower throughput\n",
                              s, (long long)slabs_[s].g.nx, (long long)slabs_[s].g.ny, (long long)slabs_[s].g.nz,
                              (long long)slabs_[s].g.Mx, (long long)slabs_[s].g.My, (long long)slabs_[s].g.Mz, xm,
@@ -906,7 +926,16 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             exchange(buffer_a, st);
         }
     };
+    // fused y-z-y pass (kx-major spectra): every convolution reads C1 and writes C2, every
+    // x pass reads C2 and writes C1, so the halo exchanges always move C1
+    const bool yzy = slabs_[s0].sp.kxl;
     auto convolve = [&](SlabState& sl, float2* Cb, const float2* K, bool fwd_done) {
+        if (yzy) {
+            T0(7);
+            engine_yzy(sl.sp, sl.C1.p, sl.C2.p, K, st);
+            T1();
+            return;
+        }
         if (band > 0 && !fwd_done) {
             T0(7);
             const bool banded = engine_convolve_banded(sl.sp, Cb, K, sl.kcompact, band, st);
@@ -929,7 +958,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     auto convolve_all = [&](bool buffer_a, int v, bool pending) {
         auto buf = [&](SlabState& sl) { return buffer_a ? sl.C1.p : sl.C2.p; };
         auto ker = [&](SlabState& sl) { return buffer_a ? sl.e1spec[v].p : sl.e2spec[v].p; };
-        bool split = pending && band <= 0;
+        bool split = pending && band <= 0 && !yzy;
         for (int s = s0; s < s1 && split; ++s)
             split = slabs_[s].sp.fy.n1 != 0 && int(slabs_[s].g.nz) > 2 * czx;
         if (split) {
@@ -969,26 +998,29 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             convolve_all(true, v, pending);
             pending = false;
             // quotient (+ forward x of the quotient) and its halo exchange
+            // (yzy: the convolution left its result in C2 and the quotient goes to C1)
+            auto qin = [&](SlabState& sl) { return yzy ? sl.C2.p : sl.C1.p; };
+            auto qout = [&](SlabState& sl) { return yzy ? sl.C1.p : sl.C2.p; };
             if (overlap) {
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    T0(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, bnd[s], st); T1();
+                    T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], st); T1();
                 }
-                xbegin(false);
+                xbegin(yzy);
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    T0(1); engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, rest[s], st); T1();
+                    T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), rest[s], st); T1();
                 }
             } else {
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
                     T0(1);
-                    engine_quotient(sl.sp, store_, sl.C1.p, sl.img[v].p, sl.C2.p, all_pairs(sl.sp), st);
+                    engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), all_pairs(sl.sp), st);
                     T1();
                 }
-                xfull(false);
+                xfull(yzy);
             }
-            convolve_all(false, v, overlap);
+            convolve_all(false, v, overlap);   // (second convolution: kernel 2; yzy: C1 -> C2)
             // update (+ forward x of the next psi) and its halo exchange
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
@@ -1060,6 +1092,7 @@ int Session::zpass_mode(int slab) const {
     SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
     if (backend_ != 0) return -1;
+    if (slabs_[slab].sp.kxl) return 4;   // fused y-z-y pass (direct z convolution inside)
     return engine_zpass_mode(slabs_[slab].sp, slabs_[slab].kcompact);
 }
 

@@ -102,7 +102,7 @@ def c2_data(gpu):
 def test_c2_4view_512_matches_oracle(gpu, c2_data):
     imgs, ws, psfs = c2_data
     psi, st, info = run_to_host(imgs, ws, psfs, PSFTYPE.INDEPENDENT, 2, 0.0)
-    assert info["zpass"] in (2, 3) and info["xpass"] == 2, info  # the fast engine passes ran
+    assert info["zpass"] in (2, 3, 4) and info["xpass"] == 2, info  # the fast engine passes ran
     himgs = [i.cpu().numpy() for i in imgs]
     hws = [w.cpu().numpy() for w in ws]
     res = ref.mv_deconvolution(himgs, hws, psfs, PSFTYPE.INDEPENDENT, 2, 0.0, precision="f32",
@@ -139,7 +139,7 @@ def test_c3_6view_1024x1024x512_tikhonov_20_iterations(gpu):
     # one slab of 1024x1024x512: spectra of 2.38 GB on the fast engine passes
     psi1, st1, info1 = run_to_host(*args)
     release()
-    assert info1["fft_dims"] == (1050, 1050, 536) and info1["zpass"] in (2, 3) and info1["xpass"] == 2, info1
+    assert info1["fft_dims"] == (1050, 1050, 536) and info1["zpass"] in (2, 3, 4) and info1["xpass"] == 2, info1
     psir, str_, _ = run_to_host(*args, fft_backend="rocfft")
     del imgs, ws
     release()
@@ -241,7 +241,7 @@ def test_c5_fp16_2048x2048x128_slab(gpu):
     psi, st, info = run_to_host(*args, storage_fp16=True)
     release()
     assert info["fft_dims"] == (2100, 2100, 152), info
-    assert info["zpass"] in (2, 3) and info["xpass"] == 2, info  # the fast engine, not Stockham
+    assert info["zpass"] in (2, 3, 4) and info["xpass"] == 2, info  # the fast engine, not Stockham
     psir, str_, _ = run_to_host(*args, storage_fp16=True, fft_backend="rocfft")
     del imgs, ws
     release()
