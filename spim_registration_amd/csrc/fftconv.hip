@@ -1225,20 +1225,30 @@ void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const fl
         const char* e = std::getenv("SPIMDECON_YZY_GRID");
         return e ? std::max(1, std::atoi(e)) : 256;
     }();
-    const unsigned grid = unsigned(std::min<int64_t>(grid_env, int64_t(a.Hx) * a.nch));
     const int KC = p.g.cz;
+    // output planes per step: 8, or 12 (SPIMDECON_YZY_G=12, A/B runs; 25-tap kernels and
+    // rings that fit the LDS only)
+    static const int g_env = [] {
+        const char* e = std::getenv("SPIMDECON_YZY_G");
+        return e && std::atoi(e) == 12 ? 12 : kYzyG;
+    }();
+    const int G = (g_env == 12 && KC == 12 && yzy_lds(int(p.g.My), 12, 12) <= 160 * 1024) ? 12 : kYzyG;
+    a.nch = int(ceil_div(p.g.nz, int64_t(G)));
+    const unsigned grid2 = unsigned(std::min<int64_t>(grid_env, int64_t(a.Hx) * a.nch));
     bool done = false;
-#define SD_YZ1(A, B, KCV)                                                                                  \
-    if (!done && p.fy.n1 == (A) && p.fy.n2 == (B) && KC == (KCV)) {                                        \
+#define SD_YZ1(A, B, KCV, GV)                                                                              \
+    if (!done && p.fy.n1 == (A) && p.fy.n2 == (B) && KC == (KCV) && G == (GV)) {                           \
         constexpr int Tv = ((A) * (B) + 63) / 64 * 64;                                                     \
-        const size_t lds = yzy_lds((A) * (B), KCV, kYzyG);                                                 \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, kYzyG, Tv>),             \
+        const size_t lds = yzy_lds((A) * (B), KCV, GV);                                                    \
+        SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "fused y-z-y ring exceeds the LDS");               \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, GV, Tv>),                \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
-        hipLaunchKernelGGL((k_yzy<A, B, KCV, kYzyG, Tv>), dim3(grid), dim3(Tv), lds, s, a);                 \
+        hipLaunchKernelGGL((k_yzy<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);                   \
         done = true;                                                                                       \
     }
-#define SD_YZ(A, B) SD_YZ1(A, B, 4) SD_YZ1(A, B, 8) SD_YZ1(A, B, 12)
+#define SD_YZ(A, B) SD_YZ1(A, B, 4, 8) SD_YZ1(A, B, 8, 8) SD_YZ1(A, B, 12, 8)
     SD_YZY_SIZES(SD_YZ)
+    SD_YZ1(20, 27, 12, 12) SD_YZ1(16, 32, 12, 12)
 #undef SD_YZ
 #undef SD_YZ1
     SD_CHECK(done, SPIMDECON_ERR_ARG, "no fused y-z-y kernel for this geometry");

@@ -223,3 +223,14 @@ def test_distinct_devices_match_single(gpu):
     assert ndev == n and devs == list(range(n))
     assert rel_l2(psi, psi1) < 1e-5
     np.testing.assert_allclose(st, st1, rtol=1e-4)
+
+
+def test_auto_slabs_keep_the_count_when_no_split_fits(gpu):
+    """One z-plane's spectrum alone past the fast passes' 32-bit offsets (33000 x 33000):
+    no z split can help, so the session keeps the caller's slab count (the Stockham
+    passes run it, as before the automatic split) instead of one-plane slabs, or 'more
+    slabs than z planes' with two devices.  Geometry only: nothing is allocated."""
+    with Session((33000, 33000, 3), slab_axis="z") as s:
+        assert s.num_slabs() == 1
+    with Session((33000, 33000, 3), devices=[0, 0], slab_axis="z") as s:
+        assert s.num_slabs() == 2
