@@ -1173,9 +1173,14 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
 #define SD_YZY_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24)
 constexpr int kYzyG = 8;
 
+// Opt-in (SPIMDECON_YZY=1): measured slower than the separate passes at 540^3 (0.81 ms
+// per fused pass against 0.68 ms for y + z + y, and the kx-major x tiles 23 % slower:
+// 8,113 vs 9,629 Mvox/s, profiles/r04_yzy_ab.txt).  One block per CU holds the 32-plane
+// ring (138 KB); its DFT phases run 3-4 of the block's 9 waves, so the pass is latency-
+// bound rather than HBM-bound.  Kept tested (bit-identical to the separate passes).
 static bool yzy_enabled() {
     const char* e = std::getenv("SPIMDECON_YZY");   // read per session (tests toggle it)
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox) {

@@ -97,7 +97,7 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
 // over kx-major spectra (p.kxl), interior planes only; Cin keeps its contents.  It
 // applies when the slab runs the direct z pass with compact kernels, the y length is
 // a two-factor length up to 576 with its ring in the LDS, cz is 4, 8 or 12, and the x
-// length has kx-major x tiles (SPIMDECON_YZY=0 turns it off).
+// length has kx-major x tiles.  Opt-in: SPIMDECON_YZY=1 (measured slower at 540^3, fftconv.hip).
 bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox);
 // compact kernel [2cz+1][My][Hp] -> kx-major [Hx][2cz+1][My]
 int64_t engine_kernel_kxmajor_elems(const SpectralPlan& p);

@@ -404,7 +404,7 @@ def test_next_value_rule_bit_exact(gpu, lam):
     ((45, 248, 248), 9, PSFTYPE.EFFICIENT_BAYESIAN, 0.006, {}),         # kc 4 (one warm-up load)
     ((30, 240, 232), 17, PSFTYPE.INDEPENDENT, 0.0, {}),                 # kc 8, plain RL update
     ((20, 516, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"storage_fp16": True}),   # My 540 = 20*27, fp16
-    ((64, 232, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"local_slabs": 2}),       # 2 z-slabs: halo exchange
+    ((64, 232, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"local_slabs": 2, "slab_axis": "z"}),  # z-slabs: halo exchange
     ((232, 64, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"local_slabs": 2, "slab_axis": "y"}),  # y-slabs
 ])
 def test_fused_yzy_pass_matches_oracle_and_column_passes(gpu, shape, ksize, psftype, lam, kw, monkeypatch):

@@ -9,3 +9,7 @@ for v in base p4; do
   tail -1 $O/strong_$v.log > $O/strong_$v.json
   python3 -c "import json; d=json.load(open('$O/strong_$v.json')); k=d['kernel_ms']; print('$v', d['value'], d['ms_per_step'], {n: k[n]['avg_ms'] for n in ('x_update','x_quotient') if n in k})"
 done
+timeout -k 10 180 ./tools/zpattern_bench > $O/zpattern.txt 2>&1 || exit 2
+timeout -k 10 300 python3 -u bench.py --steps 10 --no-cpu-baseline --no-strong-line > $O/bench.log 2>&1 || exit 3
+tail -1 $O/bench.log > $O/bench.json
+python3 -c "import json; d=json.load(open('$O/bench.json')); print('default', d['value'], d['ms_per_step'], d['config'].get('zpass_modes'))"

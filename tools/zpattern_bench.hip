@@ -26,7 +26,8 @@
 // (planar) or (p / ZB) * E * ZB + e * ZB + p % ZB (brick, SEG elements per plane run
 // become SEG * ZB contiguous elements per plane group).
 template <int DEPTH>
-__global__ __launch_bounds__(512) void k_pattern(float4* buf, long E, int P, int seg, int zb, int stagger) {
+__global__ __launch_bounds__(512) void k_pattern(float4* buf, long E, int P, int seg, int zb, int stagger,
+                                                 float4* dst = nullptr) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const long ntiles = E / seg;
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(512) void k_pattern(float4* buf, long E, int P, int
                 if (off[d] >= 0) {
                     float4 w = v[d];
                     w.x += 1.0f;
-                    buf[off[d]] = w;
+                    (dst ? dst : buf)[off[d]] = w;   // dst: out of place (read buf, write dst)
                 }
         }
     }
@@ -175,6 +176,23 @@ int main() {
     float4* dst;
     CK(hipMalloc(&dst, bytes));
     CK(hipMemset(dst, 0, bytes));
+    // the plane-strided pattern out of place (read buf, write dst: a z pass into the other buffer)
+    std::printf("out-of-place pattern: seg_bytes grid depth ms TB/s(read+write)\n");
+    for (int seg : {32, 64})
+        for (int grid : {1024, 2048}) {
+            auto launch = [&] { hipLaunchKernelGGL(k_pattern<4>, dim3(grid), dim3(512), 0, 0, buf, E, P, seg, 1, 1, dst); };
+            launch();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(a));
+            for (int r = 0; r < 10; ++r) launch();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            ms /= 10;
+            std::printf("oop %d %d 4 %.4f %.3f\n", seg * 8, grid, ms, 2.0 * bytes / (ms * 1e-3) / 1e12);
+            std::fflush(stdout);
+        }
     const long n = long(bytes / 16);
     std::printf("kind depth grid(256-thread blocks) ms TB/s(read+write)\n");
     for (int kind = 0; kind < 2; ++kind)
