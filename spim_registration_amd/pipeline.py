@@ -42,6 +42,7 @@ class TimepointResult:
     stats: np.ndarray                        # RL (iterations, views, 2)
     ms: dict = field(default_factory=dict)   # stage wall times
     engine: dict = field(default_factory=dict)   # RL FFT dims and z / x pass modes
+    stage_digests: dict = field(default_factory=dict)   # SHA-256 per stage output (digest=True)
 
 
 def apply_model(model, pts):
@@ -98,7 +99,7 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
                       threshold: float = 0.008, localization: int = 1, radius: float = 2.0,
                       blending_border=(-8, -8, -8), blending_range=(12, 12, 12),
                       weight_type=input_prep.WeightType.VIRTUAL_WEIGHTS, device: int = 0,
-                      log=None) -> TimepointResult:
+                      log=None, digest: bool = False) -> TimepointResult:
     """views: per view a [z, y, x] float32 torch tensor on the GPU (the acquired
     stack); models: 3x4 view -> world affines; bb_min / bb_dims (x, y, z)."""
     import torch
@@ -130,6 +131,12 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     beads = [p[c] if len(c) else p for p, c in zip(points, corr)]
     psfs = [tr for _, tr in psf_mod.extract_psfs(list(views), beads, psf_size, list(models), device=device)]
     t = lap("extract_psf", t)
+    sd = {}
+    if digest:   # (outside the timed stages' accounting: after the lap)
+        sd["inputs"] = _sha(b"".join(x.cpu().numpy().tobytes() for x in list(imgs) + list(ws)))
+        sd["psfs"] = _sha(b"".join(np.ascontiguousarray(p, np.float32).tobytes() for p in psfs))
+        sd["corresponding"] = _sha(b"".join(np.ascontiguousarray(c, np.int64).tobytes() for c in corr))
+        t = time.perf_counter()
     shape = tuple(imgs[0].shape)
     t_setup = t
     sess = Session((shape[2], shape[1], shape[0]), device=device)            # 4. MVDeconvolution
@@ -154,7 +161,12 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
         sess.close()
     del imgs, ws
     lap("rl_result", t)
-    return TimepointResult(psi, points, corr, psfs, stats, ms, engine)
+    return TimepointResult(psi, points, corr, psfs, stats, ms, engine, sd)
+
+
+def _sha(b: bytes) -> str:
+    import hashlib
+    return hashlib.sha256(b).hexdigest()
 
 
 class Pipeline:
@@ -169,15 +181,16 @@ class Pipeline:
     def __init__(self, **params):
         self.params = params
 
-    def process(self, views, models, bb_min, bb_dims, log=None) -> TimepointResult:
-        return process_timepoint(views, models, bb_min, bb_dims, log=log, **self.params)
+    def process(self, views, models, bb_min, bb_dims, log=None, digest=False) -> TimepointResult:
+        return process_timepoint(views, models, bb_min, bb_dims, log=log, digest=digest, **self.params)
 
 
 def result_digest(res: TimepointResult) -> dict:
     """SHA-256 of psi's bytes and of the RL statistics, plus the detection counts."""
     import hashlib
     psi = res.psi.cpu().numpy()
-    return {"psi_sha256": hashlib.sha256(psi.tobytes()).hexdigest(),
+    return {**{f"{k}_sha256": v for k, v in res.stage_digests.items()},
+            "psi_sha256": hashlib.sha256(psi.tobytes()).hexdigest(),
             "stats_sha256": hashlib.sha256(np.ascontiguousarray(res.stats, np.float64).tobytes()).hexdigest(),
             "points_sha256": hashlib.sha256(b"".join(np.ascontiguousarray(p, np.float64).tobytes()
                                                      for p in res.points)).hexdigest()}

@@ -209,12 +209,18 @@ def make_timepoint_torch(world_xyz, view_xyz, num_views: int, timepoint: int = 0
     ok = ((ip >= 1) & (ip < torch.tensor([wz - 1, wy - 1, wx - 1], device=dev))).all(dim=1)
     ip = ip[ok]
     amp = 0.5 + 0.5 * torch.rand(len(ip), generator=g, device=dev)
+    # overlapping footprints add up through atomics in an arbitrary order: accumulate the
+    # float32 terms in float64, where these few sums are exact, so the volume is the
+    # same bits on every run (tests compare a timepoint across processes)
+    beads = torch.zeros(truth.numel(), device=dev, dtype=torch.float64)
     for dz in (-1, 0, 1):
         for dy in (-1, 0, 1):
             for dx in (-1, 0, 1):
                 f = 0.55 ** (abs(dx) + abs(dy) + abs(dz))
                 idx = ((ip[:, 0] + dz) * wy + ip[:, 1] + dy) * wx + ip[:, 2] + dx
-                truth.view(-1).index_add_(0, idx, amp * f)
+                beads.index_add_(0, idx, (amp * f).double())
+    truth += beads.view_as(truth).float()
+    del beads
     vx, vy, vz = (int(v) for v in view_xyz)
     cw = ((wx - 1) / 2.0, (wy - 1) / 2.0, (wz - 1) / 2.0)
     cl = ((vx - 1) / 2.0, (vy - 1) / 2.0, (vz - 1) / 2.0)

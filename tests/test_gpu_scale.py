@@ -273,7 +273,7 @@ def test_c4_two_timepoints_back_to_back_equal_fresh_process(gpu):
     digests = []
     for t in (0, 1):
         views, models = synthetic.make_timepoint_torch((n, n, n), (n, n, n), 8, timepoint=t, device="cuda:0")
-        res = pipe.process(views, models, (0, 0, 0), (n, n, n))
+        res = pipe.process(views, models, (0, 0, 0), (n, n, n), digest=True)
         digests.append(pipeline.result_digest(res))
         print(f"  [c4x2] timepoint {t}: {res.ms}", flush=True)
         del views, res
@@ -284,5 +284,6 @@ def test_c4_two_timepoints_back_to_back_equal_fresh_process(gpu):
                         "--timepoints", "2"], capture_output=True, text=True, timeout=900, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     fresh = json.loads(r.stdout.strip().splitlines()[-1])["timepoints"][0]
-    for k in ("psi_sha256", "stats_sha256", "points_sha256"):
-        assert fresh[k] == digests[1][k], (k, fresh, digests[1])
+    keys = ("points_sha256", "corresponding_sha256", "inputs_sha256", "psfs_sha256", "stats_sha256", "psi_sha256")
+    differ = [k for k in keys if fresh[k] != digests[1][k]]   # the stages in pipeline order
+    assert not differ, differ

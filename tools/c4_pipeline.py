@@ -58,7 +58,7 @@ def main():
         torch.cuda.synchronize()
         log(f"timepoint {t}: synthetic views generated in {time.perf_counter() - tg:.1f} s")
         t0 = time.perf_counter()
-        res = pipe.process(views, models, (0, 0, 0), (n, n, n), log=log)
+        res = pipe.process(views, models, (0, 0, 0), (n, n, n), log=log, digest=a.digest)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         total += dt
