@@ -1173,11 +1173,13 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
 #define SD_YZY_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24)
 constexpr int kYzyG = 8;
 
-// Opt-in (SPIMDECON_YZY=1): measured slower than the separate passes at 540^3 (0.81 ms
-// per fused pass against 0.68 ms for y + z + y, and the kx-major x tiles 23 % slower:
-// 8,113 vs 9,629 Mvox/s, profiles/r04_yzy_ab.txt).  One block per CU holds the 32-plane
-// ring (138 KB); its DFT phases run 3-4 of the block's 9 waves, so the pass is latency-
-// bound rather than HBM-bound.  Kept tested (bit-identical to the separate passes).
+// Opt-in (SPIMDECON_YZY=1): measured slower than the separate passes at 540^3 (0.735 ms
+// per fused pass with wave-local transforms, 0.81 ms with block transforms, against 0.68
+// ms for y + z + y; the kx-major x tiles 16-23 % slower: 8,776 vs 9,827 Mvox/s,
+// profiles/r04_yzy_ab.txt).  One block per CU holds the 32-plane ring (138 KB), so the
+// pass runs 9 waves per CU and is latency-bound rather than HBM-bound (63 % of its
+// wave-cycles waiting, profiles/r04_pmc_yzy.md).  Kept tested (bit-identical to the
+// separate passes).
 static bool yzy_enabled() {
     const char* e = std::getenv("SPIMDECON_YZY");   // read per session (tests toggle it)
     return e && e[0] == '1';
@@ -1241,15 +1243,30 @@ void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const fl
     a.nch = int(ceil_div(p.g.nz, int64_t(G)));
     const unsigned grid2 = unsigned(std::min<int64_t>(grid_env, int64_t(a.Hx) * a.nch));
     bool done = false;
+    // wave-local transforms (k_yzy_wl) unless SPIMDECON_YZY_WL=0 (A/B runs)
+    static const bool wl = [] {
+        const char* e = std::getenv("SPIMDECON_YZY_WL");
+        return !(e && e[0] == '0');
+    }();
 #define SD_YZ1(A, B, KCV, GV)                                                                              \
     if (!done && p.fy.n1 == (A) && p.fy.n2 == (B) && KC == (KCV) && G == (GV)) {                           \
         constexpr int Tv = ((A) * (B) + 63) / 64 * 64;                                                     \
         const size_t lds = yzy_lds((A) * (B), KCV, GV);                                                    \
         SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "fused y-z-y ring exceeds the LDS");               \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, GV, Tv>),                \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                 \
-        hipLaunchKernelGGL((k_yzy<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);                   \
-        done = true;                                                                                       \
+        if constexpr ((GV) <= Tv / 64) {                                                                   \
+            if (wl) {                                                                                      \
+                SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy_wl<A, B, KCV, GV, Tv>),     \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));         \
+                hipLaunchKernelGGL((k_yzy_wl<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);        \
+                done = true;                                                                               \
+            }                                                                                              \
+        }                                                                                                  \
+        if (!done) {                                                                                       \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, GV, Tv>),            \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
+            hipLaunchKernelGGL((k_yzy<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);               \
+            done = true;                                                                                   \
+        }                                                                                                  \
     }
 #define SD_YZ(A, B) SD_YZ1(A, B, 4, 8) SD_YZ1(A, B, 8, 8) SD_YZ1(A, B, 12, 8)
     SD_YZY_SIZES(SD_YZ)
