@@ -443,3 +443,28 @@ def test_fused_yzy_pass_matches_oracle_and_column_passes(gpu, shape, ksize, psft
     res = ref.mv_deconvolution(imgs, ws, ks, psftype, 3, lam, precision="f32", workers=16)
     assert rel_l2(out["1"], res.psi) < TOL
     assert ((out["1"] == 0) == (res.psi == 0)).all()
+
+
+@pytest.mark.parametrize("shape,lx", [((12, 24, 516), 540), ((10, 16, 1024), 1050)])
+@pytest.mark.parametrize("psftype", [PSFTYPE.EFFICIENT_BAYESIAN, PSFTYPE.OPTIMIZATION_I])
+def test_tikhonov_update_tiles_match_oracle(gpu, shape, lx, psftype):
+    """The Tikhonov update x tiles in their voxel batches of 2 float4 per row (the
+    540-class rows of up to 5 float4 per lane, and the 1050 rows at 64 threads per
+    pair, where larger batches spilled registers) against the oracle (1e-4) and the
+    rocFFT backend (1e-5); lambda 0.006 (MVDeconvolution.java:671-705)."""
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=(9, 9, 9), partial=True, cid=41)
+    out = []
+    for backend in ("engine", "rocfft"):
+        with Session(shape[::-1], fft_backend=backend, fft_pad_policy="fast") as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(psftype)
+            s.init_psi()
+            s.run(3, 0.006)
+            s.apply_mask()
+            if backend == "engine":
+                assert s.fft_dims()[0] == lx and s.xpass_mode() == 2
+            out.append(s.get_psi())
+    assert rel_l2(out[0], out[1]) < 1e-5
+    res = ref.mv_deconvolution(imgs, ws, ks, psftype, 3, 0.006)
+    assert rel_l2(out[0], res.psi) < TOL
