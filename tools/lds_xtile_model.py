@@ -7,7 +7,8 @@ non-contiguous 16-lane groups mod 64; ds_write_b64 4x16 contiguous mod 32; ds_wr
 (max distinct addresses on one bank - 1).  Prints conflict cycles per wave and phase for
 the three modes, to compare with SQ_LDS_BANK_CONFLICT / SQ_WAVES of the PMC summary.
 
-usage: python tools/lds_xtile_model.py [N1 N2 nx] [--swap]
+usage: python tools/lds_xtile_model.py [N1 N2 nx] [--swap] [--remap]
+  --remap: also the DFT-phase lane map AM = 2 (xt_amap in fftconv_xt.inc) over pitches L+2..L+16
 """
 import sys
 from collections import defaultdict
@@ -42,9 +43,9 @@ def mirror_idx(s, n):
     return p - j if j >= n else j
 
 
-def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None):
+def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None, P=None, amap=0):
     L = N1 * N2
-    P = L + 2
+    P = L + 2 if P is None else P
     Hx = L // 2 + 1
     Hp2 = (Hx + 15) // 16 * 8
     KS = (Hp2 + TR - 1) // TR
@@ -52,7 +53,7 @@ def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None):
     nx4 = nx // 4
     if cx is None:
         cx = (L - nx) // 2
-    base = 2 * 8 * (L + 2)  # tw[L] then Z at smem + L + 2 (float2)
+    base = 8 * (L + 2)  # tw[L] then Z at smem + L + 2 (float2)
     res = defaultdict(int)
     nwaves = NP * TR // 64
     for w in range(nwaves):
@@ -68,7 +69,12 @@ def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None):
         def fft(tag):
             for l0 in [0]:
                 pass
-            cl = {l: ((w * 64 + l) % NP, (w * 64 + l) // NP) for l in lanes}
+            # xt_fft lane map: amap low bits -> r, next log2(NP) -> c, the rest -> r
+            lnp = NP.bit_length() - 1
+            cl = {}
+            for l in lanes:
+                t = w * 64 + l
+                cl[l] = ((t >> amap) & (NP - 1), (t & ((1 << amap) - 1)) | ((t >> (amap + lnp)) << amap))
             for n1 in range(N1):
                 a = {l: zaddr(c, N2 * n1 + r) for l, (c, r) in cl.items() if r < N2}
                 if a:
@@ -107,7 +113,7 @@ def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None):
                     c, hl = row_lane(l)
                     j = hl + TR * i
                     if j < nx4:
-                        qq = q ^ ((hl >> 3) & 1) if swap else q
+                        qq = q ^ (((hl >> 2) ^ (hl >> 3)) & 1) if swap else q
                         a[l] = zaddr(c, 4 * j + 2 * qq)
                 if mode != "psi":
                     res["rl rd128"] += conflicts(a, "r128")
@@ -157,7 +163,14 @@ def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None):
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     N1, N2, nx = (int(a) for a in args) if args else (20, 27, 512)
+    TR = 64 if max(N1, N2) > 32 else 32
+    L = N1 * N2
+    P0 = L + 2 + (2 if (L + 2) % 4 == 0 else 0)
     for mode in ("psi", "quot", "update"):
-        r = model(N1, N2, nx, mode, swap="--swap" in sys.argv)
+        r = model(N1, N2, nx, mode, swap="--swap" in sys.argv, TR=TR, P=P0)
         print(f"{mode:7s} total {sum(r.values()):7.1f} per wave:  " +
               ", ".join(f"{k} {v:.1f}" for k, v in sorted(r.items()) if v))
+    if "--remap" in sys.argv:
+        for P in range(L + 2, L + 18, 2):
+            r = model(N1, N2, nx, "update", swap=True, TR=TR, P=P, amap=2)
+            print(f"AM=2 pitch L+{P - L:<2d} update total {sum(r.values()):7.1f}")
