@@ -1009,7 +1009,8 @@ static int zdma_tx(int64_t Mz, int cz) {
 // instantiated set with the fewest idle output slots (nch * TR * OPT - nz), chunks of
 // H = ceil(nz / nch).  SPIMDECON_ZCHUNK=0 keeps k_zdma, =16 / =32 forces the width.
 // SPIMDECON_ZNB=3: three buffers of 32-column tiles of OPT 8 (128-plane chunks);
-// the default keeps the two-buffer candidates below.
+// the default keeps the two-buffer candidates below.  SPIMDECON_ZOPT=n keeps only the
+// candidates of OPT n (A/B runs).
 struct ZChunk { int tx = 0, opt = 0, H = 0, nb = 2; };
 static ZChunk zdmc_plan(int64_t nz, int KC) {
     const char* e = std::getenv("SPIMDECON_ZCHUNK");
@@ -1033,8 +1034,11 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
     if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
     else cands = {{32, 16}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
     int64_t bw = -1;
+    const char* eo = std::getenv("SPIMDECON_ZOPT");   // outputs per thread of the candidates (A/B runs)
+    const int fopt = eo ? std::atoi(eo) : 0;
     for (const Cand& c : cands) {
         if (force > 0 && c.tx != force) continue;
+        if (fopt > 0 && c.opt != fopt) continue;
         if (best.tx != 0 && c.tx < best.tx) break;   // the widest tile that fits wins
         const int64_t cap = int64_t(kZdThreads / c.tx) * c.opt;
         const int64_t nch = ceil_div(nz, cap);

@@ -6,7 +6,8 @@
 // SEG > 128), DEPTH pieces in flight per wave, and write each back (+1).  The layout
 // variant "brick" stores planes in groups of ZB: [P / ZB][E][ZB], so a tile's ZB
 // planes are one contiguous ZB * SEG * 8-byte run (what a z-brick layout would give).
-// usage: zpattern_bench  (prints one line per variant)
+// usage: zpattern_bench [P E [quick]]  (prints one line per variant; default P = 536, E = 540 * 272;
+//        quick: only the plane-strided 256- / 512-B variants and the contiguous references)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -114,9 +115,15 @@ __global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ src, fl
     }
 }
 
-int main() {
-    const int P = 536;
-    const long E = 540L * 272;   // multiple of every SEG below
+int main(int argc, char** argv) {
+    const int P = argc > 2 ? std::atoi(argv[1]) : 536;
+    const long E = argc > 2 ? std::atol(argv[2]) : 540L * 272;   // multiple of every SEG below
+    const bool quick = argc > 3;
+    if (E % 64 != 0) {
+        std::fprintf(stderr, "E must be a multiple of 64\n");
+        return 1;
+    }
+    std::printf("P %d planes, E %ld elements per plane (%.2f MB planes)\n", P, E, E * 8.0 / 1e6);
     const size_t bytes = size_t(P) * E * 8;
     float4* buf;
     CK(hipMalloc(&buf, bytes));
@@ -126,16 +133,20 @@ int main() {
     CK(hipEventCreate(&b));
     struct V { int seg, zb, stag, grid, depth; };
     std::vector<V> vs;
-    for (int seg : {16, 32, 64})
-        for (int stag : {1, 0})
-            for (int grid : {256, 1024})
-                vs.push_back({seg, 1, stag, grid, 4});
-    for (int seg : {16, 32})
-        for (int zb : {4, 8})
-            for (int grid : {256, 1024})
-                vs.push_back({seg, zb, 1, grid, 4});
-    vs.push_back({32, 1, 1, 256, 8});
-    vs.push_back({32, 1, 1, 256, 2});
+    if (quick) {
+        for (int seg : {32, 64}) vs.push_back({seg, 1, 1, 1024, 4});
+    } else {
+        for (int seg : {16, 32, 64})
+            for (int stag : {1, 0})
+                for (int grid : {256, 1024})
+                    vs.push_back({seg, 1, stag, grid, 4});
+        for (int seg : {16, 32})
+            for (int zb : {4, 8})
+                for (int grid : {256, 1024})
+                    vs.push_back({seg, zb, 1, grid, 4});
+        vs.push_back({32, 1, 1, 256, 8});
+        vs.push_back({32, 1, 1, 256, 2});
+    }
     std::printf("seg_bytes zbrick stagger grid depth ms TB/s(read+write)\n");
     for (const V& v : vs) {
         auto launch = [&] {
@@ -159,6 +170,7 @@ int main() {
     // plane-strided pattern at higher occupancy (grid 2048-4096 blocks of 8 waves)
     for (int seg : {32, 64})
         for (int grid : {2048, 4096}) {
+            if (quick) break;
             auto launch = [&] { hipLaunchKernelGGL(k_pattern<8>, dim3(grid), dim3(512), 0, 0, buf, E, P, seg, 1, 1); };
             launch();
             CK(hipDeviceSynchronize());
@@ -198,6 +210,7 @@ int main() {
     for (int kind = 0; kind < 2; ++kind)
         for (int depth : {1, 4, 8})
             for (int grid : {2048, 8192, 32768}) {
+                if (quick && (depth != 4 || grid != 32768)) continue;
                 auto launch = [&] {
                     if (kind == 0) {
                         if (depth == 1) hipLaunchKernelGGL(k_rmw<1>, dim3(grid), dim3(256), 0, 0, buf, n);
