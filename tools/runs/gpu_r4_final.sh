@@ -1,13 +1,18 @@
 #!/bin/bash
-# round 4 refresh: the whole -m gpu suite, smoke(), the bench line, its kernel trace and the PMC passes
+# round 4 refresh, in two calls: `tests` = the whole -m gpu suite and smoke(); `meas` = the bench
+# line, its kernel trace and the PMC passes
 export TMPDIR=/tmp
 O=gpurun_out/r4f
 mkdir -p $O
-timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rA --durations=20 --timeout 600 --timeout-method thread > $O/tests.log 2>&1
-rc=$?
-tail -3 $O/tests.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 2
+if [ "$1" != "meas" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rA --durations=20 --timeout 600 --timeout-method thread > $O/tests.log 2>&1
+  rc=$?
+  tail -3 $O/tests.log
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 2
+  tail -1 $O/smoke.log
+  exit 0
+fi
 timeout -k 10 500 python3 -u bench.py > $O/bench.log 2>&1 || exit 3
 tail -1 $O/bench.log > $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o k --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-strong-line > $O/kt.log 2>&1 || exit 4
