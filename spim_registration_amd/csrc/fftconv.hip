@@ -728,17 +728,29 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
     const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
     const int n1 = f.n1, n2 = f.n2;
+    // y passes at one block per CU (16-column tiles past 80 KB, 32 threads per column):
+    // the next tile's phase-A inputs prefetched in registers (k_col2f PF);
+    // SPIMDECON_YPF=0 keeps the plain kernel (A/B runs)
+    static const bool ypf_env = [] {
+        const char* e = std::getenv("SPIMDECON_YPF");
+        return !(e && e[0] == '0');
+    }();
+    const bool pf = ypf_env && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 && lds > size_t(80 * 1024);
     bool done = false;
+#define SD_2F_L(A, B, T, PFV)                                                                                   \
+            constexpr int TRv = SD_2F_TR(A, B);                                                                 \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv, PFV>), \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                  \
+            hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv, PFV>), dim3(grid), dim3(T * TRv), lds, s,     \
+                               p.g, p.Hp, f.tw, C, K, rbytes, tx0, ntxb, kc, uint32_t(kbytes), nout);         \
+            done = true;
 #define SD_2F_C1(A, B, T)                                                                                  \
     if constexpr (MODE < 2 || SD_2F_TR(A, B) == 32) {                                                      \
         if (!done && n1 == (A) && n2 == (B) && TX == (T)) {                                                \
-            constexpr int TRv = SD_2F_TR(A, B);                                                            \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv>), \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
-            hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv>), dim3(grid), dim3(T * TRv), lds, s,     \
-                               p.g, p.Hp, f.tw, C, K, rbytes, tx0, ntxb, kc, uint32_t(kbytes),         \
-                               nout);                                                              \
-            done = true;                                                                                   \
+            if constexpr (AXIS == 1 && MODE < 2 && (T) == 16 && SD_2F_TR(A, B) == 32 && (A) * (B) >= 640) { \
+                if (pf) { SD_2F_L(A, B, T, true) }                                                         \
+            }                                                                                              \
+            if (!done) { SD_2F_L(A, B, T, false) }                                                         \
         }                                                                                                  \
     }
 #define SD_2F_C(A, B) \
@@ -746,6 +758,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     SD_2F_SIZES(SD_2F_C)
 #undef SD_2F_C
 #undef SD_2F_C1
+#undef SD_2F_L
     SD_CHECK(done, SPIMDECON_ERR_ARG, "no two-factor column kernel for this length");
     SD_HIP(hipGetLastError());
     return true;
