@@ -730,12 +730,14 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     const int n1 = f.n1, n2 = f.n2;
     // y passes at one block per CU (16-column tiles past 80 KB, 32 threads per column):
     // the next tile's phase-A inputs prefetched in registers (k_col2f PF);
-    // SPIMDECON_YPF=0 keeps the plain kernel (A/B runs)
-    static const bool ypf_env = [] {
+    // SPIMDECON_YPF=0 keeps the plain kernel, =2 prefetches at every 16-column length of
+    // 512 points or more (A/B runs)
+    static const int ypf_env = [] {
         const char* e = std::getenv("SPIMDECON_YPF");
-        return !(e && e[0] == '0');
+        return e ? std::atoi(e) : 1;
     }();
-    const bool pf = ypf_env && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 && lds > size_t(80 * 1024);
+    const bool pf = ypf_env > 0 && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 &&
+                    (lds > size_t(80 * 1024) || (ypf_env == 2 && L >= 512));
     bool done = false;
 #define SD_2F_L(A, B, T, PFV)                                                                                   \
             constexpr int TRv = SD_2F_TR(A, B);                                                                 \
@@ -747,7 +749,7 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
 #define SD_2F_C1(A, B, T)                                                                                  \
     if constexpr (MODE < 2 || SD_2F_TR(A, B) == 32) {                                                      \
         if (!done && n1 == (A) && n2 == (B) && TX == (T)) {                                                \
-            if constexpr (AXIS == 1 && MODE < 2 && (T) == 16 && SD_2F_TR(A, B) == 32 && (A) * (B) >= 640) { \
+            if constexpr (AXIS == 1 && MODE < 2 && (T) == 16 && SD_2F_TR(A, B) == 32 && (A) * (B) >= 512) { \
                 if (pf) { SD_2F_L(A, B, T, true) }                                                         \
             }                                                                                              \
             if (!done) { SD_2F_L(A, B, T, false) }                                                         \
