@@ -1589,7 +1589,9 @@ struct DogWork {
 };
 
 std::mutex g_dogwork_mu;
-std::map<int, std::unique_ptr<DogWork>> g_dogwork;
+// never destroyed (as legacy.cpp's g_ctx): no hipFree / hipStreamDestroy from a static
+// destructor racing the HIP runtime's own teardown at process exit
+std::map<int, std::unique_ptr<DogWork>>& g_dogwork = *new std::map<int, std::unique_ptr<DogWork>>();
 
 DogWork& dog_work(int dev) {
     std::lock_guard<std::mutex> lk(g_dogwork_mu);

@@ -42,7 +42,10 @@ struct DeviceCtx {
 };
 
 std::mutex g_ctx_mu;
-std::unordered_map<int, std::unique_ptr<DeviceCtx>> g_ctx;
+// never destroyed: a static destructor would free device buffers and rocFFT plans at
+// process exit in an order relative to the HIP runtime's and rocFFT's own teardown that
+// nothing guarantees (the OS reclaims the memory)
+std::unordered_map<int, std::unique_ptr<DeviceCtx>>& g_ctx = *new std::unordered_map<int, std::unique_ptr<DeviceCtx>>();
 
 DeviceCtx& device_ctx(int dev) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);

@@ -15,7 +15,9 @@ include/spimdecon.h).  Volumes are numpy float32 arrays indexed [z, y, x]
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import weakref
 from enum import IntEnum
 
 import numpy as np
@@ -135,6 +137,18 @@ def prepare_kernels(views, iteration_type, ij_threads=8, device=None):
     return k1_out, k2_out
 
 
+# Sessions still open at interpreter exit are destroyed by an atexit handler, while the
+# library, the HIP runtime and rocFFT are all still intact -- not by __del__ during module
+# teardown, whose order relative to the other libraries' own teardown is arbitrary.
+_open_sessions: "weakref.WeakSet[Session]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_open_sessions() -> None:
+    for s in list(_open_sessions):
+        s.close()
+
+
 class Session:
     """Thin RAII wrapper of an ``mvd_session`` (GPU-resident RL state)."""
 
@@ -175,6 +189,7 @@ class Session:
                 p.device = int(devices[0])
             check(self.lib.mvd_create(C.byref(p), C.byref(h)))
         self.h = h
+        _open_sessions.add(self)
         self.params = p
         self.nviews = 0
         self.shape = (int(dims_xyz[2]), int(dims_xyz[1]), int(dims_xyz[0]))
@@ -183,6 +198,7 @@ class Session:
         if getattr(self, "h", None):
             self.lib.mvd_destroy(self.h)
             self.h = None
+            _open_sessions.discard(self)
 
     def __del__(self):
         self.close()

@@ -20,3 +20,10 @@ cp $(ls $O/kt/*/k_kernel_stats.csv $O/kt/k_kernel_stats.csv 2>/dev/null | head -
 tools/pmc_engine.sh $O/pmc || exit 5
 DIMS=$(python3 -c "import json; print(','.join(map(str, json.load(open('$O/bench.json'))['config']['fft_dims_xyz'])))") &&
 python3 tools/pmc_summary.py $O/pmc --json $O/pmc_traffic.json --dims $DIMS > $O/pmc.md
+# engine classes at the C4 and C3 geometries, and the C4 pipeline
+timeout -k 10 300 python3 bench.py --size 768 --views 8 --ksize 31 --psftype OPTIMIZATION_I --lam 0.006 --steps 3 --warmup 1 --no-cpu-baseline --no-strong-line --no-default-mode > $O/c4.log 2>&1 || exit 6
+tail -1 $O/c4.log > $O/c4.json
+timeout -k 10 300 python3 bench.py --strong --steps 3 --warmup 1 --no-cpu-baseline --no-default-mode > $O/c3.log 2>&1 || exit 7
+tail -1 $O/c3.log > $O/c3.json
+timeout -k 10 400 python3 -u tools/c4_pipeline.py > $O/c4p.log 2>&1 || exit 8
+grep '^{' $O/c4p.log | tail -1 > $O/c4p.json
