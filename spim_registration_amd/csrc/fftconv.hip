@@ -732,10 +732,8 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // the next tile's phase-A inputs prefetched in registers (k_col2f PF);
     // SPIMDECON_YPF=0 keeps the plain kernel, =2 prefetches at every 16-column length of
     // 512 points or more (A/B runs)
-    static const int ypf_env = [] {
-        const char* e = std::getenv("SPIMDECON_YPF");
-        return e ? std::atoi(e) : 1;
-    }();
+    const char* ypf_s = std::getenv("SPIMDECON_YPF");   // read per call (tests toggle it)
+    const int ypf_env = ypf_s ? std::atoi(ypf_s) : 1;
     const bool pf = ypf_env > 0 && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 &&
                     (lds > size_t(80 * 1024) || (ypf_env == 2 && L >= 512));
     bool done = false;

@@ -323,6 +323,32 @@ def test_long_columns_on_8_column_tiles(gpu, shape, ksize, env, zmode, monkeypat
     assert rel_l2(out[0], res.psi) < TOL
 
 
+@pytest.mark.parametrize("shape,my", [((8, 616, 12), 640), ((6, 776, 10), 800), ((5, 1000, 8), 1024)])
+def test_y_pass_prefetch_bit_identical(gpu, shape, my, monkeypatch):
+    """The y pass at one block per CU (16-column tiles of 640-, 800- and 1024-point
+    columns) prefetches the next tile's inputs into registers (k_col2f PF); the
+    arithmetic is the plain kernel's, so psi is bit-identical with SPIMDECON_YPF=0, and
+    both agree with the rocFFT backend (1e-5) and the oracle (1e-4)."""
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=(3, 25, 3), partial=True, cid=43)
+    out = []
+    for backend, ypf in (("engine", "1"), ("engine", "0"), ("rocfft", "1")):
+        monkeypatch.setenv("SPIMDECON_YPF", ypf)
+        with Session(shape[::-1], fft_backend=backend, fft_pad_policy="fast") as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.OPTIMIZATION_I)
+            s.init_psi()
+            s.run(3, 0.006)
+            s.apply_mask()
+            if backend == "engine":
+                assert s.fft_dims()[1] == my
+            out.append(s.get_psi())
+    assert np.array_equal(out[0], out[1])
+    assert rel_l2(out[0], out[2]) < 1e-5
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
+    assert rel_l2(out[0], res.psi) < TOL
+
+
 @pytest.mark.parametrize("shape,lx", [((6, 10, 360), 384), ((6, 10, 552), 576), ((5, 9, 776), 800)])
 def test_x_tiles_with_global_twiddles(gpu, shape, lx):
     """Row lengths whose x tiles fit one more block per CU without the LDS twiddle
