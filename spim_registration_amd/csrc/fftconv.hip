@@ -1046,21 +1046,30 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
     std::vector<Cand> cands;
     if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
     else cands = {{32, 16}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
-    int64_t bw = -1;
+    // (two blocks per CU -- 32-column tiles of 64-plane chunks or 16-column tiles of 160-
+    // plane chunks, both under 80 KB of LDS -- measured slower: C4 z pass 1.11 -> 1.41-1.54
+    // ms, 540 0.279 -> 0.398-0.413 ms; profiles/r04_zpass_two_blocks_ab.txt)
     const char* eo = std::getenv("SPIMDECON_ZOPT");   // outputs per thread of the candidates (A/B runs)
     const int fopt = eo ? std::atoi(eo) : 0;
-    for (const Cand& c : cands) {
-        if (force > 0 && c.tx != force) continue;
-        if (fopt > 0 && c.opt != fopt) continue;
-        if (best.tx != 0 && c.tx < best.tx) break;   // the widest tile that fits wins
-        const int64_t cap = int64_t(kZdThreads / c.tx) * c.opt;
-        const int64_t nch = ceil_div(nz, cap);
-        const int64_t waste = nch * cap - nz;
-        if (bw < 0 || waste < bw) {
-            best = {c.tx, c.opt, int(ceil_div(nz, nch)), 2};
-            bw = waste;
+    auto pick = [&](int opt) {
+        ZChunk b;
+        int64_t bw = -1;
+        for (const Cand& c : cands) {
+            if (force > 0 && c.tx != force) continue;
+            if (opt > 0 && c.opt != opt) continue;
+            if (b.tx != 0 && c.tx < b.tx) break;   // the widest tile that fits wins
+            const int64_t cap = int64_t(kZdThreads / c.tx) * c.opt;
+            const int64_t nch = ceil_div(nz, cap);
+            const int64_t waste = nch * cap - nz;
+            if (bw < 0 || waste < bw) {
+                b = {c.tx, c.opt, int(ceil_div(nz, nch)), 2};
+                bw = waste;
+            }
         }
-    }
+        return b;
+    };
+    best = pick(fopt);
+    if (best.tx == 0 && fopt > 0) best = pick(0);   // (no candidate of that OPT at the forced width)
     return best;
 }
 
@@ -1094,7 +1103,6 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         const int KC = zdirect_kc_bound(p.g.cz);
         const ZChunk zc = zdmc_plan(p.g.nz, KC);
         const int64_t ntiles = ceil_div(nflat, int64_t(zc.tx));
-        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256));
         const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
         const float kscale = float(p.g.Mz);
         static const int sgrp = [] {   // blocks sharing a plane order (SPIMDECON_ZSTAG_GROUP, A/B)
@@ -1107,6 +1115,11 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
             const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV));                                    \
             SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>),     \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
+            /* persistent blocks: as many per CU as are resident together (LDS and VGPRs) */             \
+            int per_cu = 1;                                                                             \
+            SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(                                        \
+                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>), kZdThreads, lds)); \
+            const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * std::max(1, per_cu)));       \
             hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, \
                                C, Kc, p.g.cz, zc.H, bytes, kscale, sgrp);                               \
             done = true;                                                                                \
