@@ -1024,7 +1024,7 @@ static int zdma_tx(int64_t Mz, int cz) {
 // SPIMDECON_ZNB=3: three buffers of 32-column tiles of OPT 8 (128-plane chunks);
 // the default keeps the two-buffer candidates below.  SPIMDECON_ZOPT=n keeps only the
 // candidates of OPT n (A/B runs).
-struct ZChunk { int tx = 0, opt = 0, H = 0, nb = 2; };
+struct ZChunk { int tx = 0, opt = 0, H = 0, nb = 2, nt = kZdThreads; };
 static ZChunk zdmc_plan(int64_t nz, int KC) {
     const char* e = std::getenv("SPIMDECON_ZCHUNK");
     const int force = e ? std::atoi(e) : -1;
@@ -1042,13 +1042,16 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
         best = {32, 8, int(ceil_div(nz, nch)), 3};
         return best;
     }
-    struct Cand { int tx, opt; };
+    struct Cand { int tx, opt, nt = kZdThreads; };
     std::vector<Cand> cands;
     if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
     else cands = {{32, 16}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
     // (two blocks per CU -- 32-column tiles of 64-plane chunks or 16-column tiles of 160-
     // plane chunks, both under 80 KB of LDS -- measured slower: C4 z pass 1.11 -> 1.41-1.54
     // ms, 540 0.279 -> 0.398-0.413 ms; profiles/r04_zpass_two_blocks_ab.txt)
+    // (1024-thread blocks of 32-column tiles at OPT 6 -- the chunk heights of OPT 12 at 512
+    // threads, 16 waves per CU under 128 VGPRs -- measured slower too: C4 1.07 -> 1.51 ms,
+    // 540 0.26 -> 0.30 ms; profiles/r04_zpass_two_blocks_ab.txt)
     const char* eo = std::getenv("SPIMDECON_ZOPT");   // outputs per thread of the candidates (A/B runs)
     const int fopt = eo ? std::atoi(eo) : 0;
     auto pick = [&](int opt) {
@@ -1058,11 +1061,11 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
             if (force > 0 && c.tx != force) continue;
             if (opt > 0 && c.opt != opt) continue;
             if (b.tx != 0 && c.tx < b.tx) break;   // the widest tile that fits wins
-            const int64_t cap = int64_t(kZdThreads / c.tx) * c.opt;
+            const int64_t cap = int64_t(c.nt / c.tx) * c.opt;
             const int64_t nch = ceil_div(nz, cap);
             const int64_t waste = nch * cap - nz;
             if (bw < 0 || waste < bw) {
-                b = {c.tx, c.opt, int(ceil_div(nz, nch)), 2};
+                b = {c.tx, c.opt, int(ceil_div(nz, nch)), 2, c.nt};
                 bw = waste;
             }
         }
@@ -1110,20 +1113,21 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
             return e ? std::max(1, std::atoi(e)) : 1;
         }();
         bool done = false;
-#define SD_ZC(KCV, OPTV, TXV, NBV)                                                                      \
-        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV)) {             \
-            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV));                                    \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>),     \
+#define SD_ZCT(KCV, OPTV, TXV, NBV, NTV)                                                                \
+        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV) && zc.nt == (NTV)) { \
+            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV, NTV));                               \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV>), \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
             /* persistent blocks: as many per CU as are resident together (LDS and VGPRs) */             \
             int per_cu = 1;                                                                             \
             SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(                                        \
-                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV>), kZdThreads, lds)); \
+                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV>), NTV, lds));   \
             const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * std::max(1, per_cu)));       \
-            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, \
+            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV, NTV>), dim3(grid), dim3(NTV), lds, s, p.g, nflat, \
                                C, Kc, p.g.cz, zc.H, bytes, kscale, sgrp);                               \
             done = true;                                                                                \
         }
+#define SD_ZC(KCV, OPTV, TXV, NBV) SD_ZCT(KCV, OPTV, TXV, NBV, kZdThreads)
 #define SD_ZC4(KCV) SD_ZC(KCV, 16, 32, 2) SD_ZC(KCV, 12, 32, 2) SD_ZC(KCV, 8, 32, 2) SD_ZC(KCV, 17, 16, 2) \
         SD_ZC(KCV, 13, 16, 2) SD_ZC(KCV, 9, 16, 2) SD_ZC(KCV, 8, 32, 3) SD_ZC(KCV, 12, 64, 2)
         SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
@@ -1131,6 +1135,7 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         SD_ZC(16, 9, 16, 2) SD_ZC(16, 8, 32, 3) SD_ZC(16, 8, 64, 2)
 #undef SD_ZC4
 #undef SD_ZC
+#undef SD_ZCT
         SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");
         SD_HIP(hipGetLastError());
         return;
