@@ -1113,29 +1113,39 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
             return e ? std::max(1, std::atoi(e)) : 1;
         }();
         bool done = false;
-#define SD_ZCT(KCV, OPTV, TXV, NBV, NTV)                                                                \
-        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV) && zc.nt == (NTV)) { \
+#define SD_ZCTK(KCV, OPTV, TXV, NBV, NTV, KDV)                                                                \
+        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV) && zc.nt == (NTV) && ((KDV) == 0 || (zkd && KC - p.g.cz == (KDV)))) { \
             const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV, NTV));                               \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV>), \
+            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
             /* persistent blocks: as many per CU as are resident together (LDS and VGPRs) */             \
             int per_cu = 1;                                                                             \
             SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(                                        \
-                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV>), NTV, lds));   \
+                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), NTV, lds));   \
             const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * std::max(1, per_cu)));       \
-            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV, NTV>), dim3(grid), dim3(NTV), lds, s, p.g, nflat, \
+            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), dim3(grid), dim3(NTV), lds, s, p.g, nflat, \
                                C, Kc, p.g.cz, zc.H, bytes, kscale, sgrp);                               \
             done = true;                                                                                \
         }
+#define SD_ZCT(KCV, OPTV, TXV, NBV, NTV) SD_ZCTK(KCV, OPTV, TXV, NBV, NTV, 0)
 #define SD_ZC(KCV, OPTV, TXV, NBV) SD_ZCT(KCV, OPTV, TXV, NBV, kZdThreads)
 #define SD_ZC4(KCV) SD_ZC(KCV, 16, 32, 2) SD_ZC(KCV, 12, 32, 2) SD_ZC(KCV, 8, 32, 2) SD_ZC(KCV, 17, 16, 2) \
         SD_ZC(KCV, 13, 16, 2) SD_ZC(KCV, 9, 16, 2) SD_ZC(KCV, 8, 32, 3) SD_ZC(KCV, 12, 64, 2)
+        // kernels of 2 KC - 1 planes in the KC layout (C4's 31-plane PSFs: KC 16) skip the two
+        // zero taps at compile time
+        // (SPIMDECON_ZKD=1 selects them, =0 or unset keeps the runtime-masked kernels; read
+        // per call)
+        const char* ezkd = std::getenv("SPIMDECON_ZKD");
+        const bool zkd = ezkd && ezkd[0] == '1';
+        SD_ZCTK(16, 12, 32, 2, kZdThreads, 1) SD_ZCTK(16, 15, 32, 2, kZdThreads, 1) SD_ZCTK(16, 8, 32, 2, kZdThreads, 1)
+        SD_ZCTK(12, 16, 32, 2, kZdThreads, 1)
         SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
         SD_ZC(16, 15, 32, 2) SD_ZC(16, 12, 32, 2) SD_ZC(16, 8, 32, 2) SD_ZC(16, 17, 16, 2) SD_ZC(16, 13, 16, 2)
         SD_ZC(16, 9, 16, 2) SD_ZC(16, 8, 32, 3) SD_ZC(16, 8, 64, 2)
 #undef SD_ZC4
 #undef SD_ZC
 #undef SD_ZCT
+#undef SD_ZCTK
         SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");
         SD_HIP(hipGetLastError());
         return;
