@@ -1133,10 +1133,10 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
         SD_ZC(KCV, 13, 16, 2) SD_ZC(KCV, 9, 16, 2) SD_ZC(KCV, 8, 32, 3) SD_ZC(KCV, 12, 64, 2)
         // kernels of 2 KC - 1 planes in the KC layout (C4's 31-plane PSFs: KC 16) skip the two
         // zero taps at compile time
-        // (SPIMDECON_ZKD=1 selects them, =0 or unset keeps the runtime-masked kernels; read
-        // per call)
+        // (C4: z pass 1.076 -> 1.046 ms, profiles/r04_zpass_tap_trim_ab.txt; SPIMDECON_ZKD=0
+        // keeps the runtime-masked kernels: A/B runs; read per call)
         const char* ezkd = std::getenv("SPIMDECON_ZKD");
-        const bool zkd = ezkd && ezkd[0] == '1';
+        const bool zkd = !(ezkd && ezkd[0] == '0');
         SD_ZCTK(16, 12, 32, 2, kZdThreads, 1) SD_ZCTK(16, 15, 32, 2, kZdThreads, 1) SD_ZCTK(16, 8, 32, 2, kZdThreads, 1)
         SD_ZCTK(12, 16, 32, 2, kZdThreads, 1)
         SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
