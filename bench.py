@@ -80,7 +80,20 @@ def parse(argv=None):
                     help="measure even when a slab runs outside the fast engine passes (else rc != 0)")
     ap.add_argument("--no-default-mode", action="store_true",
                     help="skip the second measurement in the reference default mode (OPTIMIZATION_I, 0.006)")
+    ap.add_argument("--slab-axis", default="auto", choices=["auto", "z", "y"],
+                    help="split / internal slab axis of the headline session (y: rows kept as (x, z, y), "
+                         "the layout of a y-slab rank; one GPU only unless --strong)")
+    ap.add_argument("--c5-rank", action="store_true",
+                    help="BASELINE configs[4] per rank: the 2048x256x1024 y-slab one of 8 ranks holds "
+                         "(padded 2100x1050x280 internally), fp16 img/weight storage, OPTIMIZATION_I 0.006")
     a = ap.parse_args(argv)
+    if a.c5_rank:
+        a.shape = [2048, 256, 1024]
+        a.fp16, a.slab_axis = True, "y"
+        a.psftype, a.lam = "OPTIMIZATION_I", 0.006
+        a.no_strong_line = a.no_default_mode = True
+        if a.cpu_size == 384:
+            a.cpu_size = 256
     if a.strong and a.shape is None:
         a.shape = [1024, 1024, 512]
         if a.psftype == "INDEPENDENT" and a.lam == 0.0:
@@ -106,8 +119,7 @@ def plan_gpus(args, env, visible):
 
 
 # engine kernel class -> kernel-name prefixes in the PMC table (tools/pmc_summary.py --json)
-PMC_KERNELS = {"z_convolve": ("k_zdmc<", "k_zdma<", "k_zdirect<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
-               "yzy": ("k_yzy<",),
+PMC_KERNELS = {"z_convolve": ("k_zdmc<", "k_col2f<2,", "k_colpass<2,"), "y_pass": ("k_col2f<1,", "k_colpass<1,"),
                "x_update": ("k_xtile<2,", "k_xrows<2,", "k_xpass<2,"),
                "x_quotient": ("k_xtile<1,", "k_xrows<1,", "k_xpass<1,")}
 
@@ -193,19 +205,9 @@ def engine_classes(geom, wb):
     zw = 8.0 * nzi / Mz
     zb = 8.0 + zw + kz
     yb = 8.0 * (1.0 + nzi / Mz)
-    if geom.get("yzy"):
-        # fused y-z-y pass (z pass mode 4): reads the Mz x-spectrum planes, writes the nz
-        # result planes to the other buffer, reads the kernel: the z pass's bytes, once
-        classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
-                   ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
-                   ("stats_reduce", 0, 0, 0), ("yzy", 0, 0, zb)]
-        b_view = (12 + 2 * wb) * N + (32.0 + 2 * zb) * S
-        model = (f"V*((12+2w)N + (32+2c)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
-                 f"c = fused y-z-y bytes per bin = {zb:.3f} (8 read + {zw:.3f} write + {kz:.3f} kernel)")
-        return classes, b_view, model
     classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
                ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
-               ("stats_reduce", 0, 0, 0), ("yzy_banded", 0, 0, 16 + kz)]
+               ("stats_reduce", 0, 0, 0)]
     b_view = (12 + 2 * wb) * N + (32.0 + 4 * yb + 2 * zb) * S
     model = (f"V*((12+2w)N + (32+4y+2z)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
              f"y = mean y-pass bytes per bin = {yb:.3f}, "
@@ -251,6 +253,16 @@ def timing_pass(sess, lam, views, slabs_per_group, geom, wb, fp16, backend, ms_p
             if best is None or tm[i] > best[1]:
                 best = (nm, tm[i], byts, avg)
         kernel_ms[nm] = ent
+    # SURVEY 8d's pointwise target: (20 + 2w) B per voxel and view (quotient: blurred, img,
+    # write; update: psi, integral, weight, write) over the two x-tile launches of a view
+    pointwise = None
+    if backend == "engine" and "x_quotient" in kernel_ms and "x_update" in kernel_ms:
+        tq, tu = kernel_ms["x_quotient"]["avg_ms"], kernel_ms["x_update"]["avg_ms"]
+        pb = (20 + 2 * wb) * geom["N"]
+        pointwise = {"bytes_per_view": int(pb), "t_quotient_ms": tq, "t_update_ms": tu,
+                     "achieved": round(pb / ((tq + tu) * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(pb / ((tq + tu) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "model": f"({20 + 2 * wb}*N) / (t_quotient + t_update), N = slab voxels"}
     roofline = None
     if best is not None:
         nm, _, byts, avg = best
@@ -268,7 +280,7 @@ def timing_pass(sess, lam, views, slabs_per_group, geom, wb, fp16, backend, ms_p
     it_roof = {"achieved": round(b_iter / t_iter / 1e9, 1), "peak": HBM_PEAK_GBS * geom["ngpus"],
                "unit": "GB/s", "frac": round(b_iter / t_iter / 1e9 / (HBM_PEAK_GBS * geom["ngpus"]), 4),
                "model": model, "M": list(M)}
-    return roofline, kernel_ms, it_roof
+    return roofline, kernel_ms, it_roof, pointwise
 
 
 def slab_geom(sess, nslabs, ngpus):
@@ -277,8 +289,7 @@ def slab_geom(sess, nslabs, ngpus):
     M = sess.fft_dims(0)
     ext = sess.slab_extent(0)              # internal (x, y, z) voxels of slab 0
     return {"M": M, "N": ext[0] * ext[1] * ext[2], "S": (M[0] // 2 + 1) * M[1] * M[2],
-            "nz_int": ext[2], "Mz": M[2], "kplanes": sess.kernel_planes(0), "nslabs": nslabs, "ngpus": ngpus,
-            "yzy": sess.zpass_mode(0) == 4}
+            "nz_int": ext[2], "Mz": M[2], "kplanes": sess.kernel_planes(0), "nslabs": nslabs, "ngpus": ngpus}
 
 
 def main(argv=None):
@@ -337,6 +348,10 @@ def main(argv=None):
             o0 = rank * nz
             if mode == "devices":
                 nz = nz_g
+            if args.slab_axis != "auto":
+                if N > 1 and args.slab_axis != "z":
+                    raise SystemExit("--slab-axis y stacks nothing: one GPU, or --strong")
+                axis = args.slab_axis
         imgs, ws, psfs = synthetic.make_views_torch((nz, ny, nx), args.views,
                                                     config_id=(2 if strong else 1) + rank,
                                                     ksize=(args.ksize,) * 3, device=f"cuda:{local}")
@@ -376,7 +391,7 @@ def main(argv=None):
         return max_over_ranks(t)
 
     def placement(s):
-        """devices, slabs and the engine pass each slab ran (fast: x pass 2, z pass 2/3/4);
+        """devices, slabs and the engine pass each slab ran (fast: x pass 2, z pass 3);
         a run outside the fast passes is refused unless --allow-fallback."""
         ns = s.num_slabs()
         out = {"num_devices": s.num_devices(), "slabs": ns,
@@ -384,7 +399,7 @@ def main(argv=None):
         if args.backend == "engine":
             out["xpass_modes"] = sorted({s.xpass_mode(i) for i in range(ns)})
             out["zpass_modes"] = sorted({s.zpass_mode(i) for i in range(ns)})
-            fast = out["xpass_modes"] == [2] and set(out["zpass_modes"]) <= {2, 3, 4}
+            fast = out["xpass_modes"] == [2] and out["zpass_modes"] == [3]
             if not fast and not args.allow_fallback:
                 raise SystemExit(f"engine fallback (x pass {out['xpass_modes']}, z pass {out['zpass_modes']}): "
                                  "refusing to report it; --allow-fallback to measure anyway")
@@ -398,7 +413,7 @@ def main(argv=None):
                "ms_per_step": round(t / max(steps, 1) * 1e3, 3)}
         if want_timing and not args.no_timing:
             geom = slab_geom(s, s.num_slabs(), s.num_devices())
-            out["roofline"], out["kernel_ms"], out["roofline_iteration"] = timing_pass(
+            out["roofline"], out["kernel_ms"], out["roofline_iteration"], out["pointwise"] = timing_pass(
                 s, lam, args.views, geom["nslabs"] // geom["ngpus"], geom, wb, args.fp16, args.backend,
                 out["ms_per_step"])
         return out
@@ -462,6 +477,8 @@ def main(argv=None):
                                      (f"{args.views}-view {shape[0]}^3" if len(set(shape)) == 1
                                       else f"{args.views}-view {shape[0]}x{shape[1]}x{shape[2]}")
                                      + f" per GPU (global {nx}x{ny_g}x{nz_g})")
+                                    + (" (one rank's y-slab of BASELINE configs[4], 2048x2048x1024 over 8 ranks)"
+                                       if args.c5_rank else "")
                                     + f", {args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}"),
                        "views": args.views, "volume_xyz": [nx, ny_g, nz_g], "psf": [args.ksize] * 3,
                        "fft_dims_xyz": list(M), "local_slabs": args.local_slabs,
@@ -470,6 +487,7 @@ def main(argv=None):
             "default_mode": default_mode,
             "roofline": head.get("roofline"),
             "roofline_iteration": head.get("roofline_iteration"),
+            "pointwise": head.get("pointwise"),
             "kernel_ms": head.get("kernel_ms"),
             "strong": strong,
             "cpu_baseline": cpu,

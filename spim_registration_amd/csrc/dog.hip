@@ -1709,17 +1709,17 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     const bool fused = (K == 7 || K == 15 || K == 31) && n < (int64_t(1) << 32) && d.ny <= 65535 * 32 &&
                        d.nz <= 65535;
     // (chunk + 2 + KW - 1 source planes must fit k_dog_z's kDzMaxLen plane table)
-    const int zc = std::min(kDzMaxLen - 128, std::max(1, dog_env("SPIMDECON_DOG_ZCHUNK", kDzChunk)));
-    const int ty = dog_env("SPIMDECON_DOG_XY_TY", 48) == 32 ? 32 : 48;
-    const int xcd = dog_env("SPIMDECON_DOG_XCD", 1);   // XCD-contiguous y-fastest boxes of k_dog_z
-    const int xcd_xy = dog_env("SPIMDECON_DOG_XY_XCD", 1);   // XCD-contiguous tile ranges of k_dog_xy
+    const int zc = std::min(kDzMaxLen - 128, kDzChunk);
+    constexpr int ty = 48;     // (48-row tiles: 32 measured slower)
+    constexpr int xcd = 1;     // XCD-contiguous y-fastest boxes of k_dog_z
+    constexpr int xcd_xy = 1;  // XCD-contiguous tile ranges of k_dog_xy
     // k_dog_xy: persistent blocks (3 per CU: 53.6 KB of LDS each, 16 rounds of them), tiles x fastest
     const int64_t xy_tiles = ceil_div(d.nx, kDxyTX) * ceil_div(d.ny, ty) * d.nz;
-    const dim3 gxy(unsigned(std::min<int64_t>(xy_tiles, int64_t(256) * 3 * dog_env("SPIMDECON_DOG_XY_ROUNDS", 16))));
-    // k_dog_z box: 64 x 8 (512 threads) or 64 x 16 (1024); 32 x 16 measured slower (r3i)
-    const int bx = 64, bz_y = dog_env("SPIMDECON_DOG_Z_BY", 8) == 16 ? 16 : 8;
+    const dim3 gxy(unsigned(std::min<int64_t>(xy_tiles, int64_t(256) * 3 * 16)));
+    // k_dog_z box: 64 x 8 (512 threads); 64 x 16 and 32 x 16 measured slower (r3i)
+    constexpr int bx = 64, bz_y = 8;
     // scalar plane indices (one mirror reflection: nz > K / 2; plane bytes in 31 bits)
-    const bool zsl = dog_env("SPIMDECON_DOG_Z_TBL", 0) == 0 && d.nz > K / 2 && d.nx * d.ny * 8 < (int64_t(1) << 31);
+    const bool zsl = d.nz > K / 2 && d.nx * d.ny * 8 < (int64_t(1) << 31);
     const dim3 gz(unsigned(std::max<int64_t>(1, ceil_div(d.nx - 2, bx - 2))),
                   unsigned(std::max<int64_t>(1, ceil_div(d.ny - 2, bz_y - 2))), unsigned(ceil_div(d.nz, zc)));
     bool store_dog = need_dog;
@@ -1737,14 +1737,13 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     }
     if (fused) {
         grow(w.g12, size_t(n));
-        const bool xbuf = uint64_t(n) * 4u < 0xffffffffull && dog_env("SPIMDECON_DOG_XY_BUF", 1) != 0;
+        const bool xbuf = uint64_t(n) * 4u < 0xffffffffull;
         // (k_minmax's own range: the per-value range check is skipped; SPIMDECON_DOG_MM_EXACT=0
         // keeps it -- 1.52-1.62 vs 1.66 ms per 768^3, bit-exact, gpu_r3z11.sh)
         const int mmx = !use_given && dog_env("SPIMDECON_DOG_MM_EXACT", 1) != 0 ? 1 : 0;
 #define SD_DOGXY(KV)                                                                                        \
-        if (ty == 48 && xbuf) hipLaunchKernelGGL((k_dog_xy<KV, 48, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
-        else if (ty == 48) hipLaunchKernelGGL((k_dog_xy<KV, 48, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, 32, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
+        if (xbuf) hipLaunchKernelGGL((k_dog_xy<KV, ty, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, ty, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
         SD_HIP(hipGetLastError());
@@ -1786,21 +1785,13 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
             grow(w.sink, 1);
             SD_HIP(hipMemcpyAsync(w.sink.p, &pk, sizeof(pk), hipMemcpyHostToDevice, s));   // (synchronised below)
             const int want = wmin | (wmax << 1);
-            if (dog_env("SPIMDECON_DOG_PEAKS_RING", 0)) {   // (A/B: the ring test of k_dog_z over the image)
-#define SD_DOGT4(KV, BYV) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, 64, true, true, true>), gz, dim3(64 * BYV), 0, s, d, w.g12.p, kp2(2), kinv, zc, nullptr, min_peak, want, w.sink.p, xcd, dogp);
-#define SD_DOGT(KV) if (bz_y == 16) { SD_DOGT4(KV, 16) } else { SD_DOGT4(KV, 8) }
-                if (K == 7) { SD_DOGT(7) } else if (K == 15) { SD_DOGT(15) } else { SD_DOGT(31) }
-#undef SD_DOGT
-#undef SD_DOGT4
-            } else if (d.nx >= 3 && d.ny >= 3 && d.nz >= 3) {   // (else no voxel has 26 neighbours)
-                const int zcp = std::max(1, dog_env("SPIMDECON_DOG_PEAKS_ZC", 64));
-                const int dpy = dog_env("SPIMDECON_DOG_PEAKS_Y", kDpkY) == 8 ? 8 : 4;
-                const int64_t nwave = ceil_div(d.nx - 2, int64_t(62)) * ceil_div(d.ny - 2, int64_t(dpy)) *
+            // (the ring test of k_dog_z over the stored image measured 1.19 vs 0.42 ms)
+            if (d.nx >= 3 && d.ny >= 3 && d.nz >= 3) {   // (else no voxel has 26 neighbours)
+                constexpr int zcp = 64;
+                const int64_t nwave = ceil_div(d.nx - 2, int64_t(62)) * ceil_div(d.ny - 2, int64_t(kDpkY)) *
                                       ceil_div(d.nz - 2, int64_t(zcp));
                 const dim3 gp(unsigned(ceil_div(nwave, int64_t(4))));
-                const int pxcd = dog_env("SPIMDECON_DOG_PEAKS_XCD", 1);
-                if (dpy == 8) hipLaunchKernelGGL((k_dog_peaks<8, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p, pxcd);
-                else hipLaunchKernelGGL((k_dog_peaks<4, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p, pxcd);
+                hipLaunchKernelGGL((k_dog_peaks<kDpkY, kDpkPD>), gp, dim3(256), 0, s, d, dogp, zcp, min_peak, want, w.sink.p, 1);
             }
         } else if (fused) {
             float* dst = store_dog ? dogp : nullptr;
@@ -1809,7 +1800,7 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
             const bool one = uint64_t(n) * 4u < 0x80000000ull;
             const int want = wmin | (wmax << 1);
 #define SD_DOGZ4(KV, BYV, ONEV, SLV) hipLaunchKernelGGL((k_dog_z<KV, BYV, kDzPD, 64, ONEV, SLV>), gz, dim3(64 * BYV), 0, s, d, w.g12.p, kp2(2), kinv, zc, dst, min_peak, want, w.sink.p, xcd);
-#define SD_DOGZ3(KV, ONEV, SLV) if (bz_y == 16) { SD_DOGZ4(KV, 16, ONEV, SLV) } else { SD_DOGZ4(KV, 8, ONEV, SLV) }
+#define SD_DOGZ3(KV, ONEV, SLV) SD_DOGZ4(KV, bz_y, ONEV, SLV)
 #define SD_DOGZ2(KV, ONEV) if (zsl) { SD_DOGZ3(KV, ONEV, true) } else { SD_DOGZ3(KV, ONEV, false) }
 #define SD_DOGZ(KV) if (one) { SD_DOGZ2(KV, true) } else { SD_DOGZ2(KV, false) }
             if (K == 7) { SD_DOGZ(7) } else if (K == 15) { SD_DOGZ(15) } else { SD_DOGZ(31) }

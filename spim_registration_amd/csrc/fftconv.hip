@@ -11,6 +11,8 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
+#include <cstring>
 
 namespace spimdecon {
 
@@ -434,7 +436,6 @@ constexpr int kCThreads = 1024;
 #include "fftconv_x.inc"
 #include "fftconv_xt.inc"
 #include "fftconv_zd.inc"
-#include "fftconv_yzy.inc"
 
 // ------------------------------------------------------------------ host side
 
@@ -516,90 +517,63 @@ bool x_buffer_args(const XArgs& a, Store st, const SpectralPlan& p, XArgs& b) {
     return true;
 }
 
-// k_xtile for two-factor lengths; returns the grid, 0 when it does not apply
+// k_xtile for two-factor lengths; returns the grid, 0 when it does not apply.
+// 8 row pairs per tile, one tile per block: fresh blocks keep loading while the resident
+// ones transform (quotient 0.40 vs 0.43 ms with 16 pairs and 0.45 with 4, update 0.52 vs
+// 0.58 / 0.54 ms at 540; at L = 1050 quotient 0.90 vs 1.05 ms with 16 pairs; grid-stride
+// blocks in lock step measured slower)
 template <int MODE>
 unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
-    static const bool on = [] {  // SPIMDECON_X2F=0: per-wave Stockham rows (A/B measurements)
-        const char* e = std::getenv("SPIMDECON_X2F");
-        return !(e && e[0] == '0');
-    }();
-    static const int np_env = [] {  // row pairs per tile, SPIMDECON_XTP=8|16 for A/B runs
-        const char* e = std::getenv("SPIMDECON_XTP");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 4 || v == 8 || v == 16 ? v : 0;
-    }();
-    // 8 pairs per tile (one tile per block): quotient 0.40 vs 0.43 ms with 16 pairs
-    // and 0.45 with 4, update 0.52 vs 0.58 / 0.54 ms; at L = 1050 quotient 0.90 vs 1.05 ms
-    const int L0 = int(p.g.Mx);
-    const int np = np_env == 4 && L0 != 1050 && L0 != 800 ? 8 : (np_env ? np_env : 8);
+    constexpr int NP = 8;
     XArgs b;
-    if (!on || !p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
+    if (!p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
-    const size_t lds = xt_lds(L, np, xt_twg(L, np));
+    const size_t lds = xt_lds(L, NP, xt_twg(L, NP));
     if (lds > 160 * 1024) return 0;
-    const int64_t ntiles = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, np));
-    // blocks: one tile each by default (SPIMDECON_XGRID=N caps the grid at N resident-
-    // slot rounds with grid-stride tiles, for A/B runs): fresh blocks keep loading
-    // while the resident ones transform, which grid-stride blocks in lock step do not
-    static const int64_t xrounds = [] {
-        const char* e = std::getenv("SPIMDECON_XGRID");
-        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(0);
-    }();
-    const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-    const unsigned grid = unsigned(xrounds ? std::min<int64_t>(ntiles, 256 * per_cu * xrounds) : ntiles);
+    unsigned grid = unsigned(std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(NP))));
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
-    if (p.kxl) {   // kx-major spectra (the fused y-z-y pass): 8 row pairs per tile only
-#define SD_XK(SV, A, B, TK)                                                                                     \
-        if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                                 \
-            constexpr int TRv = SD_2F_TR(A, B);                                                                 \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, 8, TRv, true>), \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(xt_lds(L, 8, xt_twg(L, 8))))); \
-            hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, 8, TRv, true>), dim3(ntiles8), dim3(8 * TRv),             \
-                               xt_lds(L, 8, xt_twg(L, 8)), s, b);                                                   \
-            done = true;                                                                                        \
-        }
-        const int64_t ntiles8 = std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(8)));
-#define SD_XK_S(A, B) SD_XK(0, A, B, false) SD_XK(1, A, B, false) if constexpr (MODE == XM_UPDATE) { SD_XK(0, A, B, true) SD_XK(1, A, B, true) }
-        SD_X2F_SIZES(SD_XK_S)
-#undef SD_XK_S
-#undef SD_XK
-        SD_CHECK(done, SPIMDECON_ERR_ARG, "no kx-major x tile for this length");
-        SD_HIP(hipGetLastError());
-        return unsigned(ntiles8);
-    }
-#define SD_XT(SV, A, B, TK, NP)                                                                            \
-    if (!done && np == NP && sv == SV && L == (A) * (B) && tik == TK) {                                   \
+#define SD_XT(SV, A, B, TK)                                                                                \
+    if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                               \
         constexpr int TRv = SD_2F_TR(A, B);                                                               \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, NP, TRv>), \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                \
-        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, NP, TRv>), dim3(grid), dim3(NP * TRv), lds, s, b); \
+        constexpr bool PFv = xt_pf((A) * (B)) && MODE != XM_PSI;                                          \
+        constexpr bool FMv = xt_fm((A) * (B)) && MODE != XM_PSI;                                          \
+        auto kfn = &k_xtile<MODE, SV, A, B, TK, NP, TRv, PFv, FMv>;                                       \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   int(lds)));                                                            \
+        if constexpr (PFv) {   /* persistent: the resident blocks stride over the tiles */              \
+            static const int per_cu = [&] {                                                               \
+                int n = 1;                                                                                \
+                SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kfn), \
+                                                                    NP * TRv, lds));                      \
+                return std::max(1, n);                                                                    \
+            }();                                                                                          \
+            grid = unsigned(std::min<int64_t>(grid, int64_t(256) * per_cu));                              \
+        }                                                                                                 \
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(NP * TRv), lds, s, b);                                   \
         done = true;                                                                                      \
     }
-    // 4 row pairs per tile for the long lengths (SPIMDECON_XTP=4, A/B): twice the
-    // independent blocks per CU at the same occupancy (the twiddle table leaves the LDS)
-#define SD_XT4(SV, A, B, TK)                                                                                \
-    if (!done && np == 4 && sv == SV && L == (A) * (B) && tik == TK) {                                    \
-        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_xtile<MODE, SV, A, B, TK, 4, SD_2F_TR(A, B)>), \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                \
-        hipLaunchKernelGGL((k_xtile<MODE, SV, A, B, TK, 4, SD_2F_TR(A, B)>), dim3(grid), dim3(4 * SD_2F_TR(A, B)), lds, s, b); \
-        done = true;                                                                                      \
-    }
-#define SD_XT4S(A, B) SD_XT4(0, A, B, false) SD_XT4(1, A, B, false) \
-    if constexpr (MODE == XM_UPDATE) { SD_XT4(0, A, B, true) SD_XT4(1, A, B, true) }
-    SD_XT4S(30, 35) SD_XT4S(25, 32)
-#undef SD_XT4S
-#undef SD_XT4
-#define SD_XT_N(A, B, NP) \
-    SD_XT(0, A, B, false, NP) SD_XT(1, A, B, false, NP) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true, NP) SD_XT(1, A, B, true, NP) }
-#define SD_XT_S(A, B) if constexpr ((A) * (B) <= 1204) { SD_XT_N(A, B, 16) } SD_XT_N(A, B, 8)
+#define SD_XT_S(A, B) \
+    SD_XT(0, A, B, false) SD_XT(1, A, B, false) if constexpr (MODE == XM_UPDATE) { SD_XT(0, A, B, true) SD_XT(1, A, B, true) }
     SD_X2F_SIZES(SD_XT_S)
 #undef SD_XT_S
-#undef SD_XT_N
 #undef SD_XT
     if (!done) return 0;
     SD_HIP(hipGetLastError());
+#if SD_XT_STAMPS
+    {
+        unsigned long long h[3][8];
+        SD_HIP(hipStreamSynchronize(s));
+        SD_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_xt_stamp), sizeof(h)));
+        const unsigned long long n = std::max(1ull, h[MODE][7]);
+        std::fprintf(stderr, "[xt_stamp] L=%d mode=%d fp16=%d tiles=%llu cycles/tile: load %llu inv %llu rl %llu fwd %llu store %llu\n",
+                     L, MODE, sv, h[MODE][7], h[MODE][0] / n, h[MODE][1] / n, h[MODE][2] / n, h[MODE][3] / n,
+                     h[MODE][4] / n);
+        std::memset(h, 0, sizeof(h));
+        SD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xt_stamp), h, sizeof(h)));
+    }
+#endif
     return grid;
 }
 
@@ -644,7 +618,6 @@ unsigned launch_x(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s
             return gt;
         }
     }
-    SD_CHECK(!p.kxl, SPIMDECON_ERR_STATE, "kx-major spectra need the x tiles (engine_yzy_ok)");
     if constexpr (MODE == XM_QUOT || MODE == XM_UPDATE) {
         if (const unsigned gr = launch_xrows<MODE>(a, st, p, s)) {
             if (MODE == XM_UPDATE) p.xmode_update = 1;
@@ -676,16 +649,8 @@ int col_tx(int L) {
 }
 
 // blocks per resident slot of the column passes (grid-stride tiles; 16 ~ one or two
-// tiles per block measured best: z 0.364 -> 0.327 ms vs 4); env
-// SPIMDECON_COLGRID overrides for A/B runs
-static int col_grid_rounds() {
-    static const int r = [] {
-        const char* e = std::getenv("SPIMDECON_COLGRID");
-        return e ? std::max(1, std::atoi(e)) : 16;
-    }();
-    return r;
-}
-#define kColGridRounds col_grid_rounds()
+// tiles per block measured best: z 0.364 -> 0.327 ms vs 4)
+constexpr int kColGridRounds = 16;
 
 // two-factor column pass; false when the buffer-offset path does not apply.
 // MODE 5: K is the compact kernel (2*kc+1 z-planes, engine_kernel_compact).
@@ -701,13 +666,8 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // the Stockham passes: L = 640 / 800 / 1024 at 32 threads, 2100 at 64)
     const int tr = (f.n1 > 32 || f.n2 > 32) ? 64 : 32;  // SD_2F_TR
     // 16-column tiles up to 160 KB (one block per CU) rather than 8-column tiles at two
-    // blocks per CU: 128-B segments won at 800 (C4 RL 815 -> 745 ms per timepoint);
-    // SPIMDECON_COL_WIDE=0 restores the 80-KB budget
-    static const bool wide = [] {
-        const char* e = std::getenv("SPIMDECON_COL_WIDE");
-        return !(e && e[0] == '0');
-    }();
-    const size_t budget = size_t(tr == 64 || wide ? 160 : 80) * 1024;
+    // blocks per CU: 128-B segments won at 800 (C4 RL 815 -> 745 ms per timepoint)
+    const size_t budget = size_t(160) * 1024;
     auto tile_lds = [&](int tx) { return size_t(L * tx + L + (MODE == 5 ? f.n2 * tx : 0)) * sizeof(float2); };
     const int TX = tile_lds(k2fTX) <= budget ? k2fTX : 8;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
@@ -729,13 +689,9 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
     const int n1 = f.n1, n2 = f.n2;
     // y passes at one block per CU (16-column tiles past 80 KB, 32 threads per column):
-    // the next tile's phase-A inputs prefetched in registers (k_col2f PF);
-    // SPIMDECON_YPF=0 keeps the plain kernel, =2 prefetches at every 16-column length of
-    // 512 points or more (A/B runs)
-    const char* ypf_s = std::getenv("SPIMDECON_YPF");   // read per call (tests toggle it)
-    const int ypf_env = ypf_s ? std::atoi(ypf_s) : 1;
-    const bool pf = ypf_env > 0 && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 &&
-                    (lds > size_t(80 * 1024) || (ypf_env == 2 && L >= 512));
+    // the next tile's phase-A inputs prefetched in registers (k_col2f PF); the plan's
+    // ypf knob (SPIMDECON_YPF=0 at plan creation) keeps the plain kernel
+    const bool pf = p.knobs.ypf && AXIS == 1 && MODE < 2 && tr == 32 && TX == 16 && lds > size_t(80 * 1024);
     bool done = false;
 #define SD_2F_L(A, B, T, PFV)                                                                                   \
             constexpr int TRv = SD_2F_TR(A, B);                                                                 \
@@ -767,12 +723,8 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
 template <int AXIS, bool INV, int ZMODE>
 void launch_col(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s,
                 int nout = -1) {
-    static const bool zk_lds = [] {  // SPIMDECON_ZK=reg: kernel spectrum in phase-B registers (A/B)
-        const char* e = std::getenv("SPIMDECON_ZK");
-        return !(e && e[0] == 'r');
-    }();
-    if constexpr (ZMODE == 1) {
-        if (f.n1 && zk_lds && launch_col2f<AXIS, 4>(p, f, C, K, s, 0, -1, 0, nout)) return;
+    if constexpr (ZMODE == 1) {   // the kernel spectrum tile in LDS, else in phase-B registers
+        if (f.n1 && launch_col2f<AXIS, 4>(p, f, C, K, s, 0, -1, 0, nout)) return;
     }
     if (f.n1 && launch_col2f<AXIS, ZMODE == 1 ? 2 : (INV ? 1 : 0)>(p, f, C, K, s, 0, -1, 0, nout)) return;
     const int tx = col_tx(f.L);
@@ -832,8 +784,28 @@ bool engine_slab_fits(int64_t nx, int64_t ny, int64_t nzs, const int halo[3], in
            uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) < kOOB;
 }
 
+// direct z convolution (fftconv_zd.inc) unless SPIMDECON_ZDIRECT=0 (read at plan creation)
+// selects the fused FFT z pass (k_col2f MODE 5)
+static bool zdirect_env() {
+    const char* e = std::getenv("SPIMDECON_ZDIRECT");
+    return !(e && e[0] == '0');
+}
+
+EngineKnobs EngineKnobs::from_env() {
+    auto off = [](const char* name) {
+        const char* e = std::getenv(name);
+        return e && e[0] == '0';
+    };
+    EngineKnobs k;
+    k.ypf = !off("SPIMDECON_YPF");
+    k.zkd = !off("SPIMDECON_ZKD");
+    k.zdirect = zdirect_env();
+    return k;
+}
+
 void SpectralPlan::create(const SlabGeom& geom, bool allow_2f, bool z_fft) {
     g = geom;
+    knobs = EngineKnobs::from_env();
     SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");
     Hx = g.Mx / 2 + 1;
     Hp = ceil_div(Hx, 16) * 16;  // column tiles of 16 (or 8/4) complex stay 128-B aligned
@@ -956,369 +928,98 @@ void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx,
     SD_HIP(hipStreamSynchronize(s));
 }
 
-// direct z convolution (fftconv_zd.inc): SPIMDECON_ZDIRECT=0 selects the fused FFT
-// z pass (k_col2f MODE 5) instead, for A/B runs and tests
-static bool zdirect_enabled() {
-    const char* e = std::getenv("SPIMDECON_ZDIRECT");  // read per call (tests toggle it)
-    return !(e && e[0] == '0');
-}
-
-// taps bound KC: 4, 8 or 12.  Measured at 540^3 against the fused FFT z pass
-// (0.30-0.31 ms): kc 4 0.258, kc 6 0.272, kc 8 0.274 ms (8 outputs per thread round);
-// kc 12 (25 taps) 0.298 ms with 4 outputs per round (0.437 with 8: the taps and
-// accumulators spilled).  Larger kernels keep the FFT z pass.
+// taps bound KC: 4, 8, 12 or 16 (33-plane kernels).  Measured at 540^3 against the fused
+// FFT z pass (0.30-0.31 ms): kc 4 0.258, kc 6 0.272, kc 8 0.274 ms; the chunked LDS-DMA
+// pass runs kc 12 (25 taps) at 0.27-0.28 ms.  Larger kernels keep the FFT z pass.
 static int zdirect_kc_bound(int kc) {
     for (int b : {4, 8, 12, 16})
         if (kc <= b) return b;
     return 0;
 }
 
-// k_zdma (LDS-DMA, double-buffered) when both buffers fit; SPIMDECON_ZDMA=0 keeps k_zdirect
-static bool zdma_enabled() {
-    const char* e = std::getenv("SPIMDECON_ZDMA");
-    return !(e && e[0] == '0');
-}
-
-// outputs per thread round: the fewest FMA + window-read slots over the rounds nz needs
-static int zdma_opt(int nz, int KC, int tx) {
-    int best = 1;
-    int64_t bc = -1;
-    // (33 taps: 17 outputs per round would spill the taps and accumulators)
-    for (int opt : {1, 5, KC > 12 ? 9 : 17}) {
-        const int rounds = tx == 16 ? zdma_rounds(nz, opt, 16) : zdma_rounds(nz, opt, 8);
-        const int64_t c = int64_t(rounds) * (2 * (2 * KC + 1) * opt + 2 * (opt + 2 * KC));
-        if (bc < 0 || c < bc) {
-            bc = c;
-            best = opt;
-        }
-    }
-    return best;
-}
-
-static size_t zdma_lds(int64_t Mz, int64_t nz, int KC, int opt, int tx) {
-    const int slots = tx == 16 ? zdma_slots(int(Mz), int(nz), KC, opt, 16) + zdma_tap_slots(KC, 16)
-                               : zdma_slots(int(Mz), int(nz), KC, opt, 8) + zdma_tap_slots(KC, 8);
-    return size_t(2) * size_t(slots) * size_t(tx) * sizeof(float2);
-}
-
-// tile width of the LDS-DMA kernel for this geometry: 16 columns when both buffers
-// fit, else 8; 0 = it does not apply (33-tap kernels run only there)
-static int zdma_tx(int64_t Mz, int cz) {
-    const int KC = zdirect_kc_bound(cz);
-    const int64_t nz = Mz - 2 * cz;
-    if (!zdma_enabled() || KC == 0 || nz < 1) return 0;
-    static const int force = [] {   // SPIMDECON_ZDMA_TX=8: 8-column tiles even when 16 fit (A/B runs)
-        const char* e = std::getenv("SPIMDECON_ZDMA_TX");
-        return e ? std::atoi(e) : 0;
-    }();
-    for (int tx : {16, 8})
-        if (force != 8 || tx == 8)
-        if (zdma_lds(Mz, nz, KC, zdma_opt(int(nz), KC, tx), tx) <= 160 * 1024) return tx;
-    return 0;
-}
-
-// k_zdmc: z chunks carried inside a block.  Tile width TX = 32 columns (256-B plane
-// segments) when its two buffers fit, else 16; OPT outputs per thread from the
-// instantiated set with the fewest idle output slots (nch * TR * OPT - nz), chunks of
-// H = ceil(nz / nch).  SPIMDECON_ZCHUNK=0 keeps k_zdma, =16 / =32 forces the width.
-// SPIMDECON_ZNB=3: three buffers of 32-column tiles of OPT 8 (128-plane chunks);
-// the default keeps the two-buffer candidates below.  SPIMDECON_ZOPT=n keeps only the
-// candidates of OPT n (A/B runs).
-struct ZChunk { int tx = 0, opt = 0, H = 0, nb = 2, nt = kZdThreads; };
+// k_zdmc: z chunks carried inside a block, 32-column tiles (256-B plane segments); OPT
+// outputs per thread from the instantiated set with the fewest idle output slots
+// (nch * TR * OPT - nz), chunks of H = ceil(nz / nch).  Measured and removed (DESIGN §4.1;
+// profiles/r03_zpattern_microbench.txt, r04_zpass_configs_ab.txt, r04_zpass_two_blocks_ab.txt):
+// whole-column tiles (k_zdma / k_zdirect: 0.285-0.29 vs 0.277 ms at 540, C4 870 -> 815 ms per
+// timepoint for the chunks), 16- and 64-column tiles, three buffers (0.318 vs 0.273 ms), two
+// blocks per CU (C4 1.11 -> 1.41-1.54 ms), 1024-thread blocks (1.07 -> 1.51 ms), stagger groups.
+struct ZChunk { int opt = 0, H = 0; };
 static ZChunk zdmc_plan(int64_t nz, int KC) {
-    const char* e = std::getenv("SPIMDECON_ZCHUNK");
-    const int force = e ? std::atoi(e) : -1;
-    const char* enb = std::getenv("SPIMDECON_ZNB");
-    const int nb = enb && std::atoi(enb) == 3 ? 3 : 2;   // 3 buffers measured slower (0.318 vs 0.273 ms)
     ZChunk best;
-    if (force == 0 || KC == 0 || nz < 1) return best;
-    if (force == 64) {   // 64-column tiles: 512-B plane segments (A/B runs)
-        const int opt = KC == 16 ? 8 : 12;
-        const int64_t nch = ceil_div(nz, int64_t(kZdThreads / 64) * opt);
-        return {64, opt, int(ceil_div(nz, nch)), 2};
-    }
-    if (nb == 3 && force != 16) {
-        const int64_t nch = ceil_div(nz, int64_t(kZdThreads / 32) * 8);
-        best = {32, 8, int(ceil_div(nz, nch)), 3};
-        return best;
-    }
-    struct Cand { int tx, opt, nt = kZdThreads; };
-    std::vector<Cand> cands;
-    if (KC == 16) cands = {{32, 15}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
-    else cands = {{32, 16}, {32, 12}, {32, 8}, {16, 17}, {16, 13}, {16, 9}};
-    // (two blocks per CU -- 32-column tiles of 64-plane chunks or 16-column tiles of 160-
-    // plane chunks, both under 80 KB of LDS -- measured slower: C4 z pass 1.11 -> 1.41-1.54
-    // ms, 540 0.279 -> 0.398-0.413 ms; profiles/r04_zpass_two_blocks_ab.txt)
-    // (1024-thread blocks of 32-column tiles at OPT 6 -- the chunk heights of OPT 12 at 512
-    // threads, 16 waves per CU under 128 VGPRs -- measured slower too: C4 1.07 -> 1.51 ms,
-    // 540 0.26 -> 0.30 ms; profiles/r04_zpass_two_blocks_ab.txt)
-    const char* eo = std::getenv("SPIMDECON_ZOPT");   // outputs per thread of the candidates (A/B runs)
-    const int fopt = eo ? std::atoi(eo) : 0;
-    auto pick = [&](int opt) {
-        ZChunk b;
-        int64_t bw = -1;
-        for (const Cand& c : cands) {
-            if (force > 0 && c.tx != force) continue;
-            if (opt > 0 && c.opt != opt) continue;
-            if (b.tx != 0 && c.tx < b.tx) break;   // the widest tile that fits wins
-            const int64_t cap = int64_t(c.nt / c.tx) * c.opt;
-            const int64_t nch = ceil_div(nz, cap);
-            const int64_t waste = nch * cap - nz;
-            if (bw < 0 || waste < bw) {
-                b = {c.tx, c.opt, int(ceil_div(nz, nch)), 2, c.nt};
-                bw = waste;
-            }
+    if (KC == 0 || nz < 1) return best;
+    int64_t bw = -1;
+    for (int opt : {KC == 16 ? 15 : 16, 12, 8}) {
+        const int64_t cap = int64_t(kZdThreads / 32) * opt;
+        const int64_t nch = ceil_div(nz, cap);
+        const int64_t waste = nch * cap - nz;
+        if (bw < 0 || waste < bw) {
+            best = {opt, int(ceil_div(nz, nch))};
+            bw = waste;
         }
-        return b;
-    };
-    best = pick(fopt);
-    if (best.tx == 0 && fopt > 0) best = pick(0);   // (no candidate of that OPT at the forced width)
+    }
     return best;
-}
-
-static size_t zdirect_lds(const SpectralPlan& p, int KC) {
-    return size_t((p.g.Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
 }
 
 bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
     const int KC = zdirect_kc_bound(cz);
     const int64_t Hp = ceil_div(Mx / 2 + 1, int64_t(16)) * 16;
-    const size_t lds = size_t((Mz + 2 * KC) * kZdPitch + (2 * KC + 1) * kZdTX) * sizeof(float2);
-    // Mz >= KC: the wrap copies of k_zdirect fill every window slot only then (a
-    // window slot left unwritten would multiply stale LDS by a zero tap: 0 * NaN)
-    return zdirect_enabled() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC && lds <= 160 * 1024 &&
-           (KC <= 12 || zdma_tx(Mz, cz) > 0) && uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
+    // Mz >= KC: a chunk's window slots (plane zc - KC + s mod Mz) wrap at most once
+    return zdirect_env() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC &&
+           uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
 }
 
 bool engine_zdirect_ok(const SpectralPlan& p) {
-    return p.Hp % kZdTX == 0 && engine_zdirect_dims_ok(p.g.Mx, p.g.My, p.g.Mz, p.g.cz);
+    return p.knobs.zdirect && p.Hp % 16 == 0 && engine_zdirect_dims_ok(p.g.Mx, p.g.My, p.g.Mz, p.g.cz);
 }
 
 int engine_zpass_mode(const SpectralPlan& p, bool compact) {
     if (!compact) return 0;
-    if (!engine_zdirect_ok(p)) return 1;
-    return (p.g.My * p.Hp) % 16 == 0 && zdmc_plan(p.g.nz, zdirect_kc_bound(p.g.cz)).tx > 0 ? 3 : 2;
+    return engine_zdirect_ok(p) ? 3 : 1;
 }
 
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s) {
-    const int64_t nflat = p.g.My * p.Hp;
-    if (engine_zdirect_ok(p) && nflat % 16 == 0 && zdmc_plan(p.g.nz, zdirect_kc_bound(p.g.cz)).tx > 0) {
-        const int KC = zdirect_kc_bound(p.g.cz);
-        const ZChunk zc = zdmc_plan(p.g.nz, KC);
-        const int64_t ntiles = ceil_div(nflat, int64_t(zc.tx));
-        const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
-        const float kscale = float(p.g.Mz);
-        static const int sgrp = [] {   // blocks sharing a plane order (SPIMDECON_ZSTAG_GROUP, A/B)
-            const char* e = std::getenv("SPIMDECON_ZSTAG_GROUP");
-            return e ? std::max(1, std::atoi(e)) : 1;
-        }();
-        bool done = false;
-#define SD_ZCTK(KCV, OPTV, TXV, NBV, NTV, KDV)                                                                \
-        if (!done && KC == (KCV) && zc.opt == (OPTV) && zc.tx == (TXV) && zc.nb == (NBV) && zc.nt == (NTV) && ((KDV) == 0 || (zkd && KC - p.g.cz == (KDV)))) { \
-            const size_t lds = size_t(zdc_lds(KCV, OPTV, TXV, NBV, NTV));                               \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));          \
-            /* persistent blocks: as many per CU as are resident together (LDS and VGPRs) */             \
-            int per_cu = 1;                                                                             \
-            SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(                                        \
-                &per_cu, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), NTV, lds));   \
-            const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * std::max(1, per_cu)));       \
-            hipLaunchKernelGGL((k_zdmc<KCV, OPTV, TXV, NBV, NTV, KDV>), dim3(grid), dim3(NTV), lds, s, p.g, nflat, \
-                               C, Kc, p.g.cz, zc.H, bytes, kscale, sgrp);                               \
-            done = true;                                                                                \
-        }
-#define SD_ZCT(KCV, OPTV, TXV, NBV, NTV) SD_ZCTK(KCV, OPTV, TXV, NBV, NTV, 0)
-#define SD_ZC(KCV, OPTV, TXV, NBV) SD_ZCT(KCV, OPTV, TXV, NBV, kZdThreads)
-#define SD_ZC4(KCV) SD_ZC(KCV, 16, 32, 2) SD_ZC(KCV, 12, 32, 2) SD_ZC(KCV, 8, 32, 2) SD_ZC(KCV, 17, 16, 2) \
-        SD_ZC(KCV, 13, 16, 2) SD_ZC(KCV, 9, 16, 2) SD_ZC(KCV, 8, 32, 3) SD_ZC(KCV, 12, 64, 2)
-        // kernels of 2 KC - 1 planes in the KC layout (C4's 31-plane PSFs: KC 16) skip the two
-        // zero taps at compile time
-        // (C4: z pass 1.076 -> 1.046 ms, profiles/r04_zpass_tap_trim_ab.txt; SPIMDECON_ZKD=0
-        // keeps the runtime-masked kernels: A/B runs; read per call)
-        const char* ezkd = std::getenv("SPIMDECON_ZKD");
-        const bool zkd = !(ezkd && ezkd[0] == '0');
-        SD_ZCTK(16, 12, 32, 2, kZdThreads, 1) SD_ZCTK(16, 15, 32, 2, kZdThreads, 1) SD_ZCTK(16, 8, 32, 2, kZdThreads, 1)
-        SD_ZCTK(12, 16, 32, 2, kZdThreads, 1)
-        SD_ZC4(4) SD_ZC4(8) SD_ZC4(12)
-        SD_ZC(16, 15, 32, 2) SD_ZC(16, 12, 32, 2) SD_ZC(16, 8, 32, 2) SD_ZC(16, 17, 16, 2) SD_ZC(16, 13, 16, 2)
-        SD_ZC(16, 9, 16, 2) SD_ZC(16, 8, 32, 3) SD_ZC(16, 8, 64, 2)
-#undef SD_ZC4
-#undef SD_ZC
-#undef SD_ZCT
-#undef SD_ZCTK
-        SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");
-        SD_HIP(hipGetLastError());
+    if (!engine_zdirect_ok(p)) {
+        const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz, int(p.g.nz));
+        SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
         return;
     }
-    if (engine_zdirect_ok(p) && zdma_tx(p.g.Mz, p.g.cz) > 0 && p.Hp % 16 == 0) {
-        const int KC = zdirect_kc_bound(p.g.cz);
-        const int tx = zdma_tx(p.g.Mz, p.g.cz);
-        const int opt = zdma_opt(int(p.g.nz), KC, tx);
-        const size_t lds = zdma_lds(p.g.Mz, p.g.nz, KC, opt, tx);
-        const int64_t ntiles = (p.Hp / tx) * p.g.My;
-        const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu));
-        const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
-        const float kscale = float(p.g.Mz);
-        bool done = false;
-#define SD_ZM(KCV, OPTV, TXV)                                                                          \
-        if (!done && KC == (KCV) && opt == (OPTV) && tx == (TXV)) {                                    \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdma<KCV, OPTV, TXV>),         \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));         \
-            hipLaunchKernelGGL((k_zdma<KCV, OPTV, TXV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, \
-                               Kc, p.g.cz, bytes, kscale);                                             \
-            done = true;                                                                               \
-        }
-#define SD_ZM2(KCV, OPTV) SD_ZM(KCV, OPTV, 16) SD_ZM(KCV, OPTV, 8)
-        SD_ZM2(4, 1) SD_ZM2(4, 5) SD_ZM2(4, 17) SD_ZM2(8, 1) SD_ZM2(8, 5) SD_ZM2(8, 17)
-        SD_ZM2(12, 1) SD_ZM2(12, 5) SD_ZM2(12, 17) SD_ZM2(16, 1) SD_ZM2(16, 5) SD_ZM2(16, 9)
-#undef SD_ZM2
-#undef SD_ZM
-        SD_CHECK(done, SPIMDECON_ERR_ARG, "no LDS-DMA z kernel for this kernel size");
-        SD_HIP(hipGetLastError());
-        return;
-    }
-    if (engine_zdirect_ok(p)) {
-        const int KC = zdirect_kc_bound(p.g.cz);
-        const size_t lds = zdirect_lds(p, KC);
-        const int64_t ntiles = (p.Hp / kZdTX) * p.g.My;
-        const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / int64_t(lds));
-        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu * kColGridRounds));
-        // per-tile ranges (k_zdirect rebuilds its resources at each tile's first column)
-        const uint32_t bytes = uint32_t(uint64_t(p.g.My * p.Hp) * p.g.Mz * sizeof(float2));
-        const uint32_t kbytes = uint32_t(uint64_t(p.g.My * p.Hp) * (2 * p.g.cz + 1) * sizeof(float2));
-        const float kscale = float(p.g.Mz);
-        bool done = false;
-#define SD_ZD(KCV)                                                                                   \
-        if (!done && KC == (KCV)) {                                                                  \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdirect<KCV, 8>),           \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));       \
-            hipLaunchKernelGGL((k_zdirect<KCV, 8>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, \
-                               C, Kc, p.g.cz, bytes, kbytes, kscale);                                \
-            done = true;                                                                             \
-        }
-        SD_ZD(4) SD_ZD(8)
-        if (!done && KC == 12) {  // 4 outputs per thread round: the 25 taps + 4 accumulators fit
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdirect<12, 4>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-            hipLaunchKernelGGL((k_zdirect<12, 4>), dim3(grid), dim3(kZdThreads), lds, s, p.g, p.Hp, C, Kc,
-                               p.g.cz, bytes, kbytes, kscale);
-            done = true;
-        }
-#undef SD_ZD
-        SD_CHECK(done, SPIMDECON_ERR_ARG, "no direct z kernel for this kernel size");
-        SD_HIP(hipGetLastError());
-        return;
-    }
-    const bool ok = launch_col2f<2, 5>(p, p.fz, C, Kc, s, 0, -1, p.g.cz, int(p.g.nz));
-    SD_CHECK(ok, SPIMDECON_ERR_ARG, "compact-kernel z pass not available");
-}
-
-// ---------------------------------------------------------------- fused y-z-y pass
-#define SD_YZY_SIZES(M) M(16, 16) M(16, 24) M(16, 32) M(20, 27) M(24, 24)
-constexpr int kYzyG = 8;
-
-// Opt-in (SPIMDECON_YZY=1): measured slower than the separate passes at 540^3 (0.735 ms
-// per fused pass with wave-local transforms, 0.81 ms with block transforms, against 0.68
-// ms for y + z + y; the kx-major x tiles 16-23 % slower: 8,776 vs 9,827 Mvox/s,
-// profiles/r04_yzy_ab.txt).  One block per CU holds the 32-plane ring (138 KB), so the
-// pass runs 9 waves per CU and is latency-bound rather than HBM-bound (63 % of its
-// wave-cycles waiting, profiles/r04_pmc_yzy.md).  Kept tested (bit-identical to the
-// separate passes).
-static bool yzy_enabled() {
-    const char* e = std::getenv("SPIMDECON_YZY");   // read per session (tests toggle it)
-    return e && e[0] == '1';
-}
-
-bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox) {
-    const int L = int(p.g.My);
-    const int KC = p.g.cz;
-    if (!yzy_enabled() || !kcompact || !zexact || p.g.Mz != p.g.nz + 2 * KC) return false;
-    if (KC != 4 && KC != 8 && KC != 12) return false;
-    bool ylen = false;
-#define SD_YL(A, B) ylen = ylen || (p.fy.n1 == (A) && p.fy.n2 == (B));
-    SD_YZY_SIZES(SD_YL)
-#undef SD_YL
-    if (!ylen || L % 2 != 0 || yzy_lds(L, KC, kYzyG) > 160 * 1024) return false;
-    // the kx-major x tiles: a two-factor x length, 16-B voxel rows, 32-bit buffer ranges
-    bool xlen = false;
-#define SD_XL(A, B) xlen = xlen || p.g.Mx == (A) * (B);
-    SD_X2F_SIZES(SD_XL)
-#undef SD_XL
-    const int Lx = int(p.g.Mx);
-    return xlen && p.fx.n1 && xt_lds(Lx, 8, xt_twg(Lx, 8)) <= 160 * 1024 && p.g.nx % 4 == 0 &&
-           uint64_t(p.spectrum_elems()) * sizeof(float2) < kOOB && uint64_t(nvox) * 4u < kOOB;
-}
-
-void engine_kernel_kxmajor(const SpectralPlan& p, const float2* Kc, float2* Kt, hipStream_t s) {
-    const int NQ = 2 * p.g.cz + 1;
-    const dim3 grid(unsigned(ceil_div(p.Hx, int64_t(32))), unsigned(ceil_div(p.g.My, int64_t(32))), unsigned(NQ));
-    hipLaunchKernelGGL(k_kernel_kxmajor, grid, dim3(256), 0, s, Kc, Kt, NQ, int(p.g.My), p.Hp, int(p.Hx));
-    SD_HIP(hipGetLastError());
-}
-
-int64_t engine_kernel_kxmajor_elems(const SpectralPlan& p) { return int64_t(2 * p.g.cz + 1) * p.g.My * p.Hx; }
-
-void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const float2* Kt, hipStream_t s) {
-    SD_CHECK(p.kxl, SPIMDECON_ERR_STATE, "the fused y-z-y pass needs kx-major spectra");
-    YzyArgs a;
-    a.Cin = Cin;
-    a.Cout = Cout;
-    a.Kt = Kt;
-    a.tw = p.fy.tw;
-    a.Hp = p.Hp;
-    a.Hx = int(p.Hx);
-    a.My = int(p.g.My);
-    a.Mz = int(p.g.Mz);
-    a.nz = int(p.g.nz);
-    a.nch = int(ceil_div(p.g.nz, int64_t(kYzyG)));
-    a.kscale = float(p.g.Mz);
-    static const int grid_env = [] {   // SPIMDECON_YZY_GRID: blocks (A/B runs; default one per CU)
-        const char* e = std::getenv("SPIMDECON_YZY_GRID");
-        return e ? std::max(1, std::atoi(e)) : 256;
-    }();
-    const int KC = p.g.cz;
-    // output planes per step: 8, or 12 (SPIMDECON_YZY_G=12, A/B runs; 25-tap kernels and
-    // rings that fit the LDS only)
-    static const int g_env = [] {
-        const char* e = std::getenv("SPIMDECON_YZY_G");
-        return e && std::atoi(e) == 12 ? 12 : kYzyG;
-    }();
-    const int G = (g_env == 12 && KC == 12 && yzy_lds(int(p.g.My), 12, 12) <= 160 * 1024) ? 12 : kYzyG;
-    a.nch = int(ceil_div(p.g.nz, int64_t(G)));
-    const unsigned grid2 = unsigned(std::min<int64_t>(grid_env, int64_t(a.Hx) * a.nch));
+    const int64_t nflat = p.g.My * p.Hp;   // a multiple of 16
+    const int KC = zdirect_kc_bound(p.g.cz);
+    const ZChunk zc = zdmc_plan(p.g.nz, KC);
+    const int64_t ntiles = ceil_div(nflat, int64_t(32));
+    const uint32_t bytes = uint32_t(uint64_t(nflat) * p.g.Mz * sizeof(float2));
+    const float kscale = float(p.g.Mz);
+    // kernels of 2 KC - 1 planes in the KC layout (C4's 31-plane PSFs: KC 16; 23-plane ones:
+    // KC 12) skip the two zero outer taps at compile time (C4: z pass 1.076 -> 1.046 ms,
+    // profiles/r04_zpass_tap_trim_ab.txt); the plan's zkd knob (SPIMDECON_ZKD=0) keeps the
+    // runtime-masked kernels
+    const int kd = p.knobs.zkd && KC - p.g.cz == 1 ? 1 : 0;
     bool done = false;
-    // wave-local transforms (k_yzy_wl) unless SPIMDECON_YZY_WL=0 (A/B runs)
-    static const bool wl = [] {
-        const char* e = std::getenv("SPIMDECON_YZY_WL");
-        return !(e && e[0] == '0');
-    }();
-#define SD_YZ1(A, B, KCV, GV)                                                                              \
-    if (!done && p.fy.n1 == (A) && p.fy.n2 == (B) && KC == (KCV) && G == (GV)) {                           \
-        constexpr int Tv = ((A) * (B) + 63) / 64 * 64;                                                     \
-        const size_t lds = yzy_lds((A) * (B), KCV, GV);                                                    \
-        SD_CHECK(lds <= 160 * 1024, SPIMDECON_ERR_ARG, "fused y-z-y ring exceeds the LDS");               \
-        if constexpr ((GV) <= Tv / 64) {                                                                   \
-            if (wl) {                                                                                      \
-                SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy_wl<A, B, KCV, GV, Tv>),     \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));         \
-                hipLaunchKernelGGL((k_yzy_wl<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);        \
-                done = true;                                                                               \
-            }                                                                                              \
-        }                                                                                                  \
-        if (!done) {                                                                                       \
-            SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_yzy<A, B, KCV, GV, Tv>),            \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));             \
-            hipLaunchKernelGGL((k_yzy<A, B, KCV, GV, Tv>), dim3(grid2), dim3(Tv), lds, s, a);               \
-            done = true;                                                                                   \
-        }                                                                                                  \
+#define SD_ZC(KCV, OPTV, KDV)                                                                                 \
+    if (!done && KC == (KCV) && zc.opt == (OPTV) && kd == (KDV)) {                                            \
+        constexpr size_t lds = size_t(zdc_lds(KCV, OPTV, 32));                                                \
+        SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, KDV>),                    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                    \
+        /* persistent blocks: as many per CU as are resident together (LDS and VGPRs), once */             \
+        static const int per_cu = [] {                                                                        \
+            int n = 1;                                                                                        \
+            SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(                                              \
+                &n, reinterpret_cast<const void*>(&k_zdmc<KCV, OPTV, KDV>), kZdThreads, lds));                \
+            return std::max(1, n);                                                                            \
+        }();                                                                                                  \
+        const unsigned grid = unsigned(std::min<int64_t>(ntiles, 256 * per_cu));                              \
+        hipLaunchKernelGGL((k_zdmc<KCV, OPTV, KDV>), dim3(grid), dim3(kZdThreads), lds, s, p.g, nflat, C, Kc,  \
+                           p.g.cz, zc.H, bytes, kscale);                                                      \
+        done = true;                                                                                          \
     }
-#define SD_YZ(A, B) SD_YZ1(A, B, 4, 8) SD_YZ1(A, B, 8, 8) SD_YZ1(A, B, 12, 8)
-    SD_YZY_SIZES(SD_YZ)
-    SD_YZ1(20, 27, 12, 12) SD_YZ1(16, 32, 12, 12)
-#undef SD_YZ
-#undef SD_YZ1
-    SD_CHECK(done, SPIMDECON_ERR_ARG, "no fused y-z-y kernel for this geometry");
+#define SD_ZC3(KCV) SD_ZC(KCV, 16, 0) SD_ZC(KCV, 12, 0) SD_ZC(KCV, 8, 0)
+    SD_ZC3(4) SD_ZC3(8) SD_ZC3(12)
+    SD_ZC(12, 16, 1) SD_ZC(12, 12, 1) SD_ZC(12, 8, 1)
+    SD_ZC(16, 15, 0) SD_ZC(16, 12, 0) SD_ZC(16, 8, 0) SD_ZC(16, 15, 1) SD_ZC(16, 12, 1) SD_ZC(16, 8, 1)
+#undef SD_ZC3
+#undef SD_ZC
+    SD_CHECK(done, SPIMDECON_ERR_ARG, "no z-chunked LDS-DMA z kernel for this kernel size");
     SD_HIP(hipGetLastError());
 }
 
@@ -1342,32 +1043,6 @@ void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t
     // as two launches (0.61 ms)
     if (K) launch_col<2, false, 1>(p, p.fz, C, K, s, int(p.g.nz));
     else launch_col<2, false, 0>(p, p.fz, C, nullptr, s);
-}
-
-int engine_band_tiles() {
-    static const int b = [] {
-        const char* e = std::getenv("SPIMDECON_BAND");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return b;
-}
-
-bool engine_convolve_banded(const SpectralPlan& p, float2* C, const float2* K, bool compact, int band,
-                            hipStream_t s) {
-    // y forward, z (forward * K * inverse) and y inverse over bands of `band` 16-bin tile
-    // columns: a band's spectrum (band * 16 * My * Mz * 8 B) stays in the Infinity Cache
-    // between the three passes, so only the first read and the last write reach HBM
-    if (band <= 0 || !p.fy.n1 || !p.fz.n1 || !K) return false;
-    const int nt = int(p.Hp / k2fTX);
-    for (int t0 = 0; t0 < nt; t0 += band) {
-        const int nb = std::min(band, nt - t0);
-        if (!launch_col2f<1, 0>(p, p.fy, C, nullptr, s, t0, nb)) return false;
-        if (!(compact ? launch_col2f<2, 5>(p, p.fz, C, K, s, t0, nb, p.g.cz)
-                      : launch_col2f<2, 4>(p, p.fz, C, K, s, t0, nb)))
-            return false;
-        if (!launch_col2f<1, 1>(p, p.fy, C, nullptr, s, t0, nb)) return false;
-    }
-    return true;
 }
 
 PairRanges all_pairs(const SpectralPlan& p) {

@@ -39,6 +39,16 @@ struct Fft1D {
     __host__ __device__ int radix(int s) const { return int((radix_packed >> (4 * s)) & 15u); }
 };
 
+// Engine knobs, read from the environment once per plan (SpectralPlan::create), so the
+// hot loop reads no environment and tests can toggle them per session:
+//   SPIMDECON_YPF=0      y passes at one block per CU without the register prefetch
+//   SPIMDECON_ZKD=0      no compile-time trim of the zero outer taps in the direct z pass
+//   SPIMDECON_ZDIRECT=0  the fused FFT z pass (k_col2f MODE 5) instead of the direct one
+struct EngineKnobs {
+    bool ypf = true, zkd = true, zdirect = true;
+    static EngineKnobs from_env();
+};
+
 // per-slab engine state (twiddles, row maps)
 struct SpectralPlan {
     SlabGeom g{};
@@ -50,8 +60,7 @@ struct SpectralPlan {
     // x pass the last update launch ran: 2 = two-factor tiles (k_xtile), 1 = per-wave
     // rows (k_xrows), 0 = Stockham rows (k_xpass); -1 = none yet (mvd_xpass_mode)
     mutable int xmode_update = -1;
-    // kx-major spectra C[z][kx][y] (the fused y-z-y pass, engine_yzy); else C[z][y][kx]
-    bool kxl = false;
+    EngineKnobs knobs;
     int64_t spectrum_elems() const { return Hp * g.My * g.Mz; }
     // allow_2f: use the two-factor register kernels for lengths in the fast-path table
     // z_fft = false: no z transform plan (the direct z convolution needs none, and then
@@ -87,22 +96,12 @@ bool engine_zdirect_ok(const SpectralPlan& p);
 // sizes Mz = nz + 2 cz exactly)
 bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz);
 // z pass of a slab: 0 = fused FFT with full kernel spectra, 1 = fused FFT with
-// compact kernels, 2 = direct convolution with compact kernels
+// compact kernels, 3 = direct convolution with compact kernels (z chunks, k_zdmc)
 int engine_zpass_mode(const SpectralPlan& p, bool compact);
 int64_t engine_kernel_compact_elems(const SpectralPlan& p);
 void engine_kernel_compact(const SpectralPlan& p, const float* d_kernel, int kx, int ky, int kz, float scale,
                            float2* work, float2* Kc, hipStream_t s);
 void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hipStream_t s);
-// Fused y-z-y pass (fftconv_yzy.inc): Cout = y-inverse(z-convolve(y-forward(Cin), Kt))
-// over kx-major spectra (p.kxl), interior planes only; Cin keeps its contents.  It
-// applies when the slab runs the direct z pass with compact kernels, the y length is
-// a two-factor length up to 576 with its ring in the LDS, cz is 4, 8 or 12, and the x
-// length has kx-major x tiles.  Opt-in: SPIMDECON_YZY=1 (measured slower at 540^3, fftconv.hip).
-bool engine_yzy_ok(const SpectralPlan& p, bool kcompact, bool zexact, int64_t nvox);
-// compact kernel [2cz+1][My][Hp] -> kx-major [Hx][2cz+1][My]
-int64_t engine_kernel_kxmajor_elems(const SpectralPlan& p);
-void engine_kernel_kxmajor(const SpectralPlan& p, const float2* Kc, float2* Kt, hipStream_t s);
-void engine_yzy(const SpectralPlan& p, const float2* Cin, float2* Cout, const float2* Kt, hipStream_t s);
 // Y pass: in-place complex FFT along y (inverse when inv)
 void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 // Forward y pass of the z planes [z0, z1) only (false: not available for this plan,
@@ -110,12 +109,6 @@ void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 bool engine_ypass_planes(const SpectralPlan& p, float2* C, int z0, int z1, hipStream_t s);
 // Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
-// y forward + z convolve + y inverse over bands of `band` tile columns (Infinity-Cache
-// resident); false (nothing launched) when the two-factor path does not apply.
-// engine_band_tiles(): the band width from env SPIMDECON_BAND (0 = unbanded)
-bool engine_convolve_banded(const SpectralPlan& p, float2* C, const float2* K, bool compact, int band,
-                            hipStream_t s);
-int engine_band_tiles();
 // packed row pairs (rows 2i, 2i+1 of the My*Mz padded rows) an x pass covers:
 // [b0, b0 + n0) then [b1, b1 + n1)
 struct PairRanges {

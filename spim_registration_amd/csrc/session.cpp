@@ -458,28 +458,8 @@ void Session::build_spectra() {
                     (which == 0 ? sl.e1spec : sl.e2spec).push_back(std::move(spec));
                 }
             }
-            // the fused y-z-y pass: kx-major spectra and kernels (the compact kernels are
-            // replaced by their kx-major transposes; no other pass reads them then)
-            sl.sp.kxl = engine_yzy_ok(sl.sp, sl.kcompact, sl.zexact, sl.n);
-            if (sl.sp.kxl) {
-                for (auto* ks : {&sl.e1spec, &sl.e2spec})
-                    for (auto& k : *ks) {
-                        DBuf<float2> kt(size_t(engine_kernel_kxmajor_elems(sl.sp)));
-                        engine_kernel_kxmajor(sl.sp, k.p, kt.p, stream_);
-                        SD_HIP(hipStreamSynchronize(stream_));
-                        k = std::move(kt);
-                    }
-            }
         }
         SD_HIP(hipStreamSynchronize(stream_));
-    }
-    if (backend_ == 0) {   // one layout for every slab (the exchanges copy whole planes)
-        bool any = false, all = true;
-        for (auto& sl : slabs_) {
-            any = any || sl.sp.kxl;
-            all = all && sl.sp.kxl;
-        }
-        SD_CHECK(any == all, SPIMDECON_ERR_STATE, "slabs disagree on the fused y-z-y pass");
     }
     spectra_ready_ = true;
 }
@@ -748,20 +728,20 @@ void Session::run(int iters, double lambda, double* stats) {
         if (slabs_.size() > 1 || p_.nranks > 1) poisoned_ = true;
         throw;
     }
-    static const bool verbose = [] {
+    static const bool quiet = [] {
         const char* e = std::getenv("SPIMDECON_VERBOSE");
-        return e && e[0] && e[0] != '0';
+        return e && e[0] == '0';
     }();
-    if (backend_ == 0 && verbose && !warned_fallback_) {
+    if (backend_ == 0 && !quiet && !warned_fallback_) {
         // the fast paths are a layout choice, not a semantic one: a slab outside them runs
         // the Stockham passes with the same results, several times slower -- say so once
-        // when asked (SPIMDECON_VERBOSE=1; callers can query mvd_xpass_mode / mvd_zpass_mode)
+        // (SPIMDECON_VERBOSE=0 silences it; callers can query mvd_xpass_mode / mvd_zpass_mode)
         for (int s = 0; s < int(slabs_.size()); ++s) {
             const int xm = slabs_[s].sp.xmode_update, zm = zpass_mode(s);
-            if (xm != 2 || (zm != 2 && zm != 3 && zm != 4)) {
+            if (xm != 2 || zm != 3) {
                 std::fprintf(stderr,
                              "[spimdecon] warning: slab %d (%lld x %lld x %lld, padded %lld x %lld x %lld) runs "
-                             "outside the fast engine passes (x pass %d, z pass %d; fast = 2 and 2/3/4): same "
+                             "outside the fast engine passes (x pass %d, z pass %d; fast = 2 and 3): same "
                              "results, lower throughput\n",
                              s, (long long)slabs_[s].g.nx, (long long)slabs_[s].g.ny, (long long)slabs_[s].g.nz,
                              (long long)slabs_[s].g.Mx, (long long)slabs_[s].g.My, (long long)slabs_[s].g.Mz, xm,
@@ -884,9 +864,8 @@ void Session::run_rocfft(int iters, double lambda) {
     }
 }
 
-// timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 fused z pass,
-// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce, 7 banded y-z-y convolve
-// (recorded by group 0 only)
+// timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 z pass,
+// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce (recorded by group 0 only)
 void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     const int V = nviews_;
     DevGroup& gr = groups_[gi];
@@ -895,7 +874,6 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     const bool tm = gi == 0;
     auto T0 = [&](int cls) { if (tm) tstart(cls, st); };
     auto T1 = [&]() { if (tm) tstop(st); };
-    const int band = engine_band_tiles();
     const bool halo = slabs_.size() > 1 || p_.nranks > 1;
     // overlap: the x pass writes the planes the neighbours need first; their exchange
     // (xstream) runs while the x pass covers the rest of the slab
@@ -926,22 +904,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             exchange(buffer_a, st);
         }
     };
-    // fused y-z-y pass (kx-major spectra): every convolution reads C1 and writes C2, every
-    // x pass reads C2 and writes C1, so the halo exchanges always move C1
-    const bool yzy = slabs_[s0].sp.kxl;
     auto convolve = [&](SlabState& sl, float2* Cb, const float2* K, bool fwd_done) {
-        if (yzy) {
-            T0(7);
-            engine_yzy(sl.sp, sl.C1.p, sl.C2.p, K, st);
-            T1();
-            return;
-        }
-        if (band > 0 && !fwd_done) {
-            T0(7);
-            const bool banded = engine_convolve_banded(sl.sp, Cb, K, sl.kcompact, band, st);
-            T1();
-            if (banded) return;
-        }
         if (!fwd_done) { T0(2); engine_ypass(sl.sp, Cb, false, st); T1(); }
         T0(3);
         if (sl.kcompact) engine_zpass_compact(sl.sp, Cb, K, st);
@@ -958,7 +921,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     auto convolve_all = [&](bool buffer_a, int v, bool pending) {
         auto buf = [&](SlabState& sl) { return buffer_a ? sl.C1.p : sl.C2.p; };
         auto ker = [&](SlabState& sl) { return buffer_a ? sl.e1spec[v].p : sl.e2spec[v].p; };
-        bool split = pending && band <= 0 && !yzy;
+        bool split = pending;
         for (int s = s0; s < s1 && split; ++s)
             split = slabs_[s].sp.fy.n1 != 0 && int(slabs_[s].g.nz) > 2 * czx;
         if (split) {
@@ -997,16 +960,15 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             const bool last = (it == iters - 1) && (v == V - 1);
             convolve_all(true, v, pending);
             pending = false;
-            // quotient (+ forward x of the quotient) and its halo exchange
-            // (yzy: the convolution left its result in C2 and the quotient goes to C1)
-            auto qin = [&](SlabState& sl) { return yzy ? sl.C2.p : sl.C1.p; };
-            auto qout = [&](SlabState& sl) { return yzy ? sl.C1.p : sl.C2.p; };
+            // quotient (+ forward x of the quotient: C1 -> C2) and its halo exchange
+            auto qin = [&](SlabState& sl) { return sl.C1.p; };
+            auto qout = [&](SlabState& sl) { return sl.C2.p; };
             if (overlap) {
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
                     T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], st); T1();
                 }
-                xbegin(yzy);
+                xbegin(false);
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
                     T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), rest[s], st); T1();
@@ -1018,9 +980,9 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                     engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), all_pairs(sl.sp), st);
                     T1();
                 }
-                xfull(yzy);
+                xfull(false);
             }
-            convolve_all(false, v, overlap);   // (second convolution: kernel 2; yzy: C1 -> C2)
+            convolve_all(false, v, overlap);   // (second convolution: kernel 2)
             // update (+ forward x of the next psi) and its halo exchange
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
@@ -1092,7 +1054,6 @@ int Session::zpass_mode(int slab) const {
     SD_CHECK(slab >= 0 && slab < int(slabs_.size()), SPIMDECON_ERR_ARG, "bad slab");
     SD_CHECK(spectra_ready_, SPIMDECON_ERR_STATE, "not initialised");
     if (backend_ != 0) return -1;
-    if (slabs_[slab].sp.kxl) return 4;   // fused y-z-y pass (direct z convolution inside)
     return engine_zpass_mode(slabs_[slab].sp, slabs_[slab].kcompact);
 }
 

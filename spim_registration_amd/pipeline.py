@@ -133,9 +133,10 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     t = lap("extract_psf", t)
     sd = {}
     if digest:   # (outside the timed stages' accounting: after the lap)
-        sd["inputs"] = _sha(b"".join(x.cpu().numpy().tobytes() for x in list(imgs) + list(ws)))
-        sd["psfs"] = _sha(b"".join(np.ascontiguousarray(p, np.float32).tobytes() for p in psfs))
-        sd["corresponding"] = _sha(b"".join(np.ascontiguousarray(c, np.int64).tobytes() for c in corr))
+        # one volume on the host at a time (a C4 timepoint is 16 volumes of 768^3 float32)
+        sd["inputs"] = _sha(x.cpu().numpy() for x in list(imgs) + list(ws))
+        sd["psfs"] = _sha(np.ascontiguousarray(p, np.float32) for p in psfs)
+        sd["corresponding"] = _sha(np.ascontiguousarray(c, np.int64) for c in corr)
         t = time.perf_counter()
     shape = tuple(imgs[0].shape)
     t_setup = t
@@ -164,9 +165,13 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     return TimepointResult(psi, points, corr, psfs, stats, ms, engine, sd)
 
 
-def _sha(b: bytes) -> str:
+def _sha(parts) -> str:
+    """SHA-256 of the concatenated bytes of `parts` (arrays), fed one part at a time."""
     import hashlib
-    return hashlib.sha256(b).hexdigest()
+    h = hashlib.sha256()
+    for a in parts:
+        h.update(memoryview(np.ascontiguousarray(a)).cast("B"))
+    return h.hexdigest()
 
 
 class Pipeline:

@@ -235,7 +235,7 @@ def test_compact_kernel_z_pass(gpu, shape, ksize, monkeypatch):
     (SPIMDECON_ZK=full) and the oracle."""
     imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
     out = []
-    for zk, zd, mode in (("compact", "1", (2, 3)), ("compact", "0", (1,)), ("full", "1", (0,))):
+    for zk, zd, mode in (("compact", "1", (3,)), ("compact", "0", (1,)), ("full", "1", (0,))):
         monkeypatch.setenv("SPIMDECON_ZK", zk)
         monkeypatch.setenv("SPIMDECON_ZDIRECT", zd)
         with Session(shape[::-1], fft_pad_policy="fast") as s:
@@ -263,33 +263,47 @@ def test_compact_kernel_z_pass(gpu, shape, ksize, monkeypatch):
                                          ((512, 13, 12), (3, 3, 25)),     # 2 chunks of 256, My odd: half tile
                                          ((770, 9, 12), (3, 3, 31))])     # 33 taps, 4 chunks of 193
 def test_direct_z_pass_lds_dma(gpu, shape, ksize, monkeypatch):
-    """The LDS-DMA direct z passes -- k_zdmc (mode 3, the default): z chunks of 32- or
-    16-column tiles carried inside one block; k_zdma (SPIMDECON_ZCHUNK=0): whole 16-
-    or 8-column tiles -- against the full kernel spectra and the oracle; for kernels
-    up to 25 planes also against the register-staged k_zdirect (SPIMDECON_ZDMA=0)."""
+    """The LDS-DMA direct z pass (k_zdmc, mode 3): z chunks of 32-column tiles carried
+    inside one block, against the full kernel spectra and the oracle."""
     imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
-    runs = [("compact", "1", "-1", (3,)), ("full", "1", "-1", (0,)), ("compact", "1", "16", (3,)),
-            ("compact", "1", "0", (2,))]
-    if ksize[2] <= 25:
-        runs.append(("compact", "0", "0", (2,)))
     out = []
-    for zk, dma, chunk, mode in runs:
+    for zk, mode in (("compact", 3), ("full", 0)):
         monkeypatch.setenv("SPIMDECON_ZK", zk)
-        monkeypatch.setenv("SPIMDECON_ZDMA", dma)
-        monkeypatch.setenv("SPIMDECON_ZCHUNK", chunk)
         with Session(shape[::-1], fft_pad_policy="fast") as s:
             for i, w, k in zip(imgs, ws, ks):
                 s.add_view(i, w, k)
             s.init(PSFTYPE.OPTIMIZATION_I)
-            assert s.zpass_mode() in mode
+            assert s.zpass_mode() == mode
             s.init_psi()
             s.run(3, 0.006)
             s.apply_mask()
             out.append(s.get_psi())
     assert not np.array_equal(out[0], out[1]), "direct path not taken (identical bits)"
     assert rel_l2(out[0], out[1]) < 1e-5
-    for o in out[2:]:
-        assert rel_l2(out[0], o) < 1e-6
+    res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
+    assert rel_l2(out[0], res.psi) < TOL
+
+
+@pytest.mark.parametrize("shape,ksize", [((200, 10, 12), (3, 3, 23)),    # kc 11 in the KC-12 layout
+                                         ((300, 10, 12), (3, 5, 31))])   # kc 15 in the KC-16 layout
+def test_z_tap_trim_bit_identical(gpu, shape, ksize, monkeypatch):
+    """Kernels of 2 KC - 1 planes skip the two zero outer taps of the KC layout at compile
+    time (k_zdmc KD = 1); the skipped products are exact zeros, so psi is bit-identical to
+    the runtime-masked kernel (SPIMDECON_ZKD=0) and on the oracle."""
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True, cid=44)
+    out = []
+    for zkd in ("1", "0"):
+        monkeypatch.setenv("SPIMDECON_ZKD", zkd)
+        with Session(shape[::-1], fft_pad_policy="fast") as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(PSFTYPE.OPTIMIZATION_I)
+            assert s.zpass_mode() == 3
+            s.init_psi()
+            s.run(3, 0.006)
+            s.apply_mask()
+            out.append(s.get_psi())
+    assert np.array_equal(out[0], out[1])
     res = ref.mv_deconvolution(imgs, ws, ks, PSFTYPE.OPTIMIZATION_I, 3, 0.006)
     assert rel_l2(out[0], res.psi) < TOL
 
@@ -297,11 +311,11 @@ def test_direct_z_pass_lds_dma(gpu, shape, ksize, monkeypatch):
 @pytest.mark.parametrize("shape,ksize,env,zmode", [
     ((20, 776, 12), (3, 25, 3), {}, 3),                               # My 800 = 25*32: 8-column y tiles
     ((616, 8, 12), (3, 3, 25), {"SPIMDECON_ZDIRECT": "0"}, 1),        # Mz 640: compact FFT z, 8-column tiles
-    ((770, 8, 12), (3, 3, 31), {"SPIMDECON_ZCHUNK": "0"}, 2)])        # Mz 800: 33-tap k_zdma, 8-column tiles
+    ((770, 8, 12), (3, 3, 31), {}, 3)])                               # Mz 800: 33-tap chunked direct z
 def test_long_columns_on_8_column_tiles(gpu, shape, ksize, env, zmode, monkeypatch):
     """Two-factor lengths whose 16-column tile exceeds the 80-KB budget of 32 threads
     per column (640, 800, 1024) run 8-column tiles instead of the Stockham passes;
-    33-tap kernels on long columns run the LDS-DMA z pass with 8-column tiles."""
+    33-tap kernels on long columns run the chunked LDS-DMA z pass."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
@@ -420,55 +434,6 @@ def test_next_value_rule_bit_exact(gpu, lam):
     nan = np.isnan(want)
     assert np.array_equal(np.isnan(got), nan)
     assert np.array_equal(got[~nan].view(np.uint32), want[~nan].view(np.uint32))
-
-
-# ---------------------------------------------------------------- fused y-z-y pass (z pass mode 4)
-
-@pytest.mark.parametrize("shape,ksize,psftype,lam,kw", [
-    ((40, 232, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {}),            # My 256 = 16*16, kc 12, 5 full chunks
-    ((37, 360, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {}),            # My 384, last chunk of 5 planes
-    ((45, 248, 248), 9, PSFTYPE.EFFICIENT_BAYESIAN, 0.006, {}),         # kc 4 (one warm-up load)
-    ((30, 240, 232), 17, PSFTYPE.INDEPENDENT, 0.0, {}),                 # kc 8, plain RL update
-    ((20, 516, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"storage_fp16": True}),   # My 540 = 20*27, fp16
-    ((64, 232, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"local_slabs": 2, "slab_axis": "z"}),  # z-slabs: halo exchange
-    ((232, 64, 232), 25, PSFTYPE.OPTIMIZATION_I, 0.006, {"local_slabs": 2, "slab_axis": "y"}),  # y-slabs
-])
-def test_fused_yzy_pass_matches_oracle_and_column_passes(gpu, shape, ksize, psftype, lam, kw, monkeypatch):
-    """The fused y-z-y pass over kx-major spectra (one read and one write of every bin per
-    convolution; fftconv_yzy.inc) against the oracle (1e-4) and against the separate
-    y / direct-z / y passes over the x-fastest layout (SPIMDECON_YZY=0, 1e-5; observed:
-    bit-identical, the same arithmetic in the same order): several
-    y lengths and kernel half sizes, a partial last chunk of output planes, fp16 storage,
-    the Tikhonov and plain updates, z- and y-slabs with their halo exchanges."""
-    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=(ksize,) * 3, partial=True, cid=31)
-    out, stats = {}, {}
-    for yzy in ("1", "0"):
-        monkeypatch.setenv("SPIMDECON_YZY", yzy)
-        with Session(shape[::-1], **kw) as s:
-            for i, w, k in zip(imgs, ws, ks):
-                s.add_view(i, w, k)
-            s.init(psftype)
-            modes = {s.zpass_mode(j) for j in range(s.num_slabs())}
-            if yzy == "1":
-                assert modes == {4}, modes
-            else:
-                assert modes <= {2, 3}, modes
-            s.init_psi()
-            stats[yzy] = s.run(3, lam)
-            s.apply_mask()
-            assert {s.xpass_mode(j) for j in range(s.num_slabs())} == {2}
-            out[yzy] = s.get_psi()
-    # the fused pass runs the same arithmetic as the separate passes (the same two-factor
-    # y transforms, the same tap order of the direct z convolution): equal bits so far;
-    # which path ran is pinned by the z pass modes above
-    assert rel_l2(out["1"], out["0"]) < 1e-5
-    np.testing.assert_allclose(stats["1"], stats["0"], rtol=1e-4)
-    if kw.get("storage_fp16"):
-        imgs = [i.astype(np.float16).astype(np.float32) for i in imgs]
-        ws = [w.astype(np.float16).astype(np.float32) for w in ws]
-    res = ref.mv_deconvolution(imgs, ws, ks, psftype, 3, lam, precision="f32", workers=16)
-    assert rel_l2(out["1"], res.psi) < TOL
-    assert ((out["1"] == 0) == (res.psi == 0)).all()
 
 
 @pytest.mark.parametrize("shape,lx", [((12, 24, 516), 540), ((10, 16, 1024), 1050)])

@@ -115,6 +115,64 @@ __global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ src, fl
     }
 }
 
+// Round-5 references (the round-4 copy topped out at 5.54 TB/s against the
+// guide's ~6.3): one-shot blocks (no grid stride), 32-bit float4 indices, no per-element
+// test (n_eff is a whole number of chunks), DEPTH independent 16-B loads per thread in
+// flight, 256-thread blocks -- enough resident waves per SIMD to cover HBM latency.
+template <int DEPTH>
+__global__ __launch_bounds__(256) void k_copy2(const float4* __restrict__ src, float4* __restrict__ dst) {
+    const uint32_t base = blockIdx.x * uint32_t(DEPTH * 256) + threadIdx.x;
+    float4 v[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) v[d] = src[base + d * 256];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) dst[base + d * 256] = v[d];
+}
+template <int DEPTH>
+__global__ __launch_bounds__(256) void k_rmw2(float4* buf) {
+    const uint32_t base = blockIdx.x * uint32_t(DEPTH * 256) + threadIdx.x;
+    float4 v[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) v[d] = buf[base + d * 256];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        v[d].x += 1.0f;
+        buf[base + d * 256] = v[d];
+    }
+}
+// the z pass's plane-strided shape with the same hygiene: one block per tile of SEG
+// elements x P planes, 1-KiB pieces (wave-uniform tail test only), 32-bit offsets
+template <int DEPTH, int SEG>
+__global__ __launch_bounds__(512) void k_pattern2(float4* buf, uint32_t E, int P) {
+    constexpr int bytes_tile_plane = SEG * 8;
+    constexpr int lseg = __builtin_ctz(bytes_tile_plane);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x;
+    const int npieces = (bytes_tile_plane * P) >> 10;
+    const int stag = int((tile * 2654435761u) % uint32_t(npieces));
+    for (int j0 = wave * DEPTH; j0 < npieces; j0 += 8 * DEPTH) {
+        float4 v[DEPTH];
+        uint32_t off[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            int j = j0 + d < npieces ? j0 + d : j0;   // (wave-uniform)
+            j += stag;
+            if (j >= npieces) j -= npieces;
+            const int b = (j * 64 + lane) * 16;
+            off[d] = (uint32_t(b >> lseg) * E * 8u + tile * uint32_t(bytes_tile_plane) + uint32_t(b & (bytes_tile_plane - 1))) >> 4;
+            v[d] = buf[off[d]];
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            if (j0 + d < npieces) {
+                v[d].x += 1.0f;
+                buf[off[d]] = v[d];
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int P = argc > 2 ? std::atoi(argv[1]) : 536;
     const long E = argc > 2 ? std::atol(argv[2]) : 540L * 272;   // multiple of every SEG below
@@ -235,6 +293,53 @@ int main(int argc, char** argv) {
                             2.0 * bytes / (ms * 1e-3) / 1e12);
                 std::fflush(stdout);
             }
+    // round-5 references
+    std::printf("round-5 references: kind depth blocks ms TB/s(read+write)\n");
+    auto timeit = [&](auto&& launch, double moved) {
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        for (int r = 0; r < 10; ++r) launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ms /= 10;
+        return std::make_pair(ms, moved / (ms * 1e-3) / 1e12);
+    };
+    for (int depth : {2, 4, 8}) {
+        const uint32_t chunk = uint32_t(depth) * 256;
+        const uint32_t blocks = uint32_t(n / chunk);
+        const double moved = 2.0 * double(blocks) * chunk * 16;
+        for (int kind = 0; kind < 2; ++kind) {
+            auto r = timeit([&] {
+                if (kind == 0) {
+                    if (depth == 2) hipLaunchKernelGGL(k_copy2<2>, dim3(blocks), dim3(256), 0, 0, buf, dst);
+                    else if (depth == 4) hipLaunchKernelGGL(k_copy2<4>, dim3(blocks), dim3(256), 0, 0, buf, dst);
+                    else hipLaunchKernelGGL(k_copy2<8>, dim3(blocks), dim3(256), 0, 0, buf, dst);
+                } else {
+                    if (depth == 2) hipLaunchKernelGGL(k_rmw2<2>, dim3(blocks), dim3(256), 0, 0, buf);
+                    else if (depth == 4) hipLaunchKernelGGL(k_rmw2<4>, dim3(blocks), dim3(256), 0, 0, buf);
+                    else hipLaunchKernelGGL(k_rmw2<8>, dim3(blocks), dim3(256), 0, 0, buf);
+                }
+            }, moved);
+            std::printf("%s2 %d %u %.4f %.3f\n", kind == 0 ? "copy" : "rmw", depth, blocks, r.first, r.second);
+            std::fflush(stdout);
+        }
+    }
+    std::printf("round-5 plane-strided pattern: seg_bytes depth tiles ms TB/s(read+write)\n");
+    for (int seg : {16, 32, 64}) {
+        const uint32_t tiles = uint32_t(E / seg);
+        for (int depth : {4, 8}) {
+            auto r = timeit([&] {
+#define PAT(D, S) if (depth == D && seg == S) hipLaunchKernelGGL((k_pattern2<D, S>), dim3(tiles), dim3(512), 0, 0, buf, uint32_t(E), P);
+                PAT(4, 16) PAT(8, 16) PAT(4, 32) PAT(8, 32) PAT(4, 64) PAT(8, 64)
+#undef PAT
+            }, 2.0 * double(bytes));
+            std::printf("pat2 %d %d %u %.4f %.3f\n", seg * 8, depth, tiles, r.first, r.second);
+            std::fflush(stdout);
+        }
+    }
     CK(hipFree(dst));
     CK(hipFree(buf));
     return 0;
