@@ -207,7 +207,7 @@ def engine_classes(geom, wb):
     yb = 8.0 * (1.0 + nzi / Mz)
     classes = [("x_update", 8 + wb, N, 16), ("x_quotient", wb, N, 16), ("y_pass", 0, 0, yb),
                ("z_convolve", 0, 0, zb), ("x_forward_psi", 4, N, 8), ("halo_exchange", 0, 0, 0),
-               ("stats_reduce", 0, 0, 0)]
+               ("stats_reduce", 0, 0, 0), ("exchange_window", 0, 0, 0)]
     b_view = (12 + 2 * wb) * N + (32.0 + 4 * yb + 2 * zb) * S
     model = (f"V*((12+2w)N + (32+4y+2z)S) B/iter, S = (Mx/2+1)*My*Mz, w = img/weight bytes, "
              f"y = mean y-pass bytes per bin = {yb:.3f}, "

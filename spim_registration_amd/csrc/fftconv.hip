@@ -994,7 +994,7 @@ void engine_zpass_compact(const SpectralPlan& p, float2* C, const float2* Kc, hi
     // KC 12) skip the two zero outer taps at compile time (C4: z pass 1.076 -> 1.046 ms,
     // profiles/r04_zpass_tap_trim_ab.txt); the plan's zkd knob (SPIMDECON_ZKD=0) keeps the
     // runtime-masked kernels
-    const int kd = p.knobs.zkd && KC - p.g.cz == 1 ? 1 : 0;
+    const int kd = p.knobs.zkd && (KC == 12 || KC == 16) && KC - p.g.cz == 1 ? 1 : 0;   // (instantiated there)
     bool done = false;
 #define SD_ZC(KCV, OPTV, KDV)                                                                                 \
     if (!done && KC == (KCV) && zc.opt == (OPTV) && kd == (KDV)) {                                            \

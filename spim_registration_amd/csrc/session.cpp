@@ -551,6 +551,21 @@ void Session::tstop(hipStream_t st) {
     tcur_ = -1;
 }
 
+void Session::wstart(hipStream_t st) {
+    if (!timing_on_) return;
+    TimingRec r{7, get_event(), nullptr};
+    SD_HIP(hipEventRecord(r.a, st));
+    trecs_.push_back(r);
+    wcur_ = int(trecs_.size()) - 1;
+}
+
+void Session::wstop(hipStream_t st) {
+    if (!timing_on_ || wcur_ < 0) return;
+    trecs_[wcur_].b = get_event();
+    SD_HIP(hipEventRecord(trecs_[wcur_].b, st));
+    wcur_ = -1;
+}
+
 void Session::timing(double* out16) {
     for (int i = 0; i < 16; ++i) out16[i] = tacc_[i];
 }
@@ -865,7 +880,8 @@ void Session::run_rocfft(int iters, double lambda) {
 }
 
 // timing classes: 0 update x-pass, 1 quotient x-pass, 2 y passes, 3 z pass,
-// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce (recorded by group 0 only)
+// 4 initial psi x-pass, 5 halo exchange, 6 stats reduce, 7 overlap window of an
+// overlapped exchange (recorded by group 0 only)
 void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     const int V = nviews_;
     DevGroup& gr = groups_[gi];
@@ -881,7 +897,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     bool overlap = halo;
     for (int s = s0; s < s1; ++s) overlap = overlap && split_pairs(slabs_[s], bnd[s], rest[s]);
     // exchange of one buffer: begin after the boundary launches, end before the y pass
-    auto xbegin = [&](bool buffer_a) {
+    auto xbegin = [&](bool buffer_a, bool window = true) {
         if (bar) {
             group_exchange_begin(gi, buffer_a, *bar);
         } else {
@@ -890,15 +906,17 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             exchange(buffer_a, gr.xstream);
             SD_HIP(hipEventRecord(gr.ev_x, gr.xstream));
         }
+        if (tm && window) wstart(st);
     };
     auto xend = [&]() {
+        if (tm) wstop(st);   // (no-op after an unwindowed begin)
         if (bar) group_exchange_end(gi);
         else SD_HIP(hipStreamWaitEvent(st, gr.ev_x, 0));
     };
     auto xfull = [&](bool buffer_a) {  // not overlapped
         if (!halo) return;
         if (bar) {
-            xbegin(buffer_a);
+            xbegin(buffer_a, false);
             xend();
         } else {
             exchange(buffer_a, st);

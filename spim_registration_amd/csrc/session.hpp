@@ -162,6 +162,11 @@ private:
     void allreduce_max(double* host, int n);
     void tstart(int cls, hipStream_t st = nullptr);
     void tstop(hipStream_t st = nullptr);
+    // class 7: the overlap window of a halo exchange -- the compute stream's work queued
+    // between the exchange's start and the wait for it (group 0's stream)
+    void wstart(hipStream_t st);
+    void wstop(hipStream_t st);
+    int wcur_ = -1;
 
     mvd_params p_{};        // internal geometry (dims / halo with y and z swapped when axis_ == 1)
     int64_t odims_[3] = {0, 0, 0};  // this rank's volume in the caller's layout {nx, ny, nz}
