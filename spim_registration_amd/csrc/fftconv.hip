@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 
@@ -567,9 +568,9 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
         SD_HIP(hipStreamSynchronize(s));
         SD_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_xt_stamp), sizeof(h)));
         const unsigned long long n = std::max(1ull, h[MODE][7]);
-        std::fprintf(stderr, "[xt_stamp] L=%d mode=%d fp16=%d tiles=%llu cycles/tile: load %llu inv %llu rl %llu fwd %llu store %llu\n",
+        std::fprintf(stderr, "[xt_stamp] L=%d mode=%d fp16=%d tiles=%llu cycles/tile: load %llu inv %llu rl %llu fwd %llu store %llu prologue %llu\n",
                      L, MODE, sv, h[MODE][7], h[MODE][0] / n, h[MODE][1] / n, h[MODE][2] / n, h[MODE][3] / n,
-                     h[MODE][4] / n);
+                     h[MODE][4] / n, h[MODE][5] / n);
         std::memset(h, 0, sizeof(h));
         SD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xt_stamp), h, sizeof(h)));
     }
