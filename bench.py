@@ -244,6 +244,10 @@ def timing_pass(sess, lam, views, slabs_per_group, geom, wb, fp16, backend, ms_p
             # with a halo exchange the forward y pass runs as plane ranges around the
             # exchange wait (3 launches): count whole-volume passes, 4 per view and slab
             cnt = min(cnt, 4 * views * 2 * max(1, slabs_per_group))
+        if nm in ("x_update", "x_quotient") and backend == "engine":
+            # overlapped exchanges split an x pass into the boundary pairs and the rest
+            # (2 launches): count whole-slab passes, 1 per view and slab
+            cnt = min(cnt, views * 2 * max(1, slabs_per_group))
         avg = tm[i] / cnt
         ent = {"total_ms": round(tm[i], 4), "launches": cnt, "avg_ms": round(avg, 5)}
         byts = bvox * nv + bspec * S

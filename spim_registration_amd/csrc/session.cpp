@@ -595,6 +595,24 @@ bool Session::split_pairs(const SlabState& sl, PairRanges& bnd, PairRanges& rest
     rest.n0 = int(s2 - e1);
     rest.b1 = int(e2);
     rest.n1 = int(npairs - e2);
+    // Halo planes the neighbours provide ([nz, nz + cz) from the upper one, [Mz - cz, Mz)
+    // from the lower one) are skip rows: the x pass would transform zeros and store
+    // nothing there, so their pairs are left out (an interior slab of C3's 8-rank split:
+    // 24 of 152 planes).  Halo planes at the global boundary are mirror rows and stay.
+    if (sl.g.Mz == nz + 2 * cz) {
+        const bool hi_skip = sl.g.z0 + nz < sl.g.nzg;   // an upper neighbour exists
+        const bool lo_skip = sl.g.z0 > 0;               // a lower neighbour exists
+        const int64_t m0 = ((nz + cz) * My) / 2;             // first pair touching plane nz + cz
+        const int64_t m1 = ceil_div((nz + cz) * My, int64_t(2));   // pairs past plane nz + cz - 1
+        if (hi_skip && lo_skip) {
+            rest.n1 = 0;
+        } else if (hi_skip) {
+            rest.b1 = int(m0);
+            rest.n1 = int(npairs - m0);
+        } else if (lo_skip) {
+            rest.n1 = int(m1 - e2);
+        }
+    }
     return true;
 }
 

@@ -50,3 +50,24 @@ def test_engine_iteration_model_bytes():
     assert y == pytest.approx(8.0 * (1 + 128 / 152))
     z = dict((c[0], c) for c in classes)["z_convolve"][3]
     assert z == pytest.approx(8.0 + 8.0 * 128 / 152 + 8.0 * 25 / 152)
+
+
+def test_c5_rank_preset():
+    """--c5-rank: one rank's y-slab of BASELINE configs[4] (2048 x 256 x 1024, fp16
+    img / weights, OPTIMIZATION_I 0.006) as the headline, no extra lines."""
+    a = bench.parse(["--c5-rank"])
+    assert a.shape == [2048, 256, 1024] and a.fp16 and a.slab_axis == "y"
+    assert (a.psftype, a.lam) == ("OPTIMIZATION_I", 0.006)
+    assert a.no_strong_line and a.no_default_mode
+
+
+def test_engine_classes_pointwise_bytes():
+    """The iteration model counts (12 + 2w) N + (32 + 4y + 2z) S bytes per view; the
+    exchange-window class carries no bytes (it is a time, not a pass)."""
+    geom = {"N": 1000, "S": 600, "nz_int": 10, "Mz": 12, "kplanes": 5}
+    classes, b_view, _ = bench.engine_classes(geom, 2)
+    names = [c[0] for c in classes]
+    assert names[7] == "exchange_window" and classes[7][1:] == (0, 0, 0)
+    yb = 8.0 * (1 + 10 / 12)
+    zb = 8.0 + 8.0 * 10 / 12 + 8.0 * 5 / 12
+    assert abs(b_view - ((12 + 4) * 1000 + (32 + 4 * yb + 2 * zb) * 600)) < 1e-6
