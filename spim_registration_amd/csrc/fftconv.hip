@@ -537,22 +537,21 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
 #define SD_XT(SV, A, B, TK)                                                                                \
     if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                               \
-        constexpr int TRv = xt_tr(A, B);                                                               \
+        constexpr int TRv = SD_2F_TR(A, B);                                                               \
         constexpr bool PFv = xt_pf((A) * (B)) && MODE != XM_PSI;                                          \
-        constexpr bool FMv = xt_fm((A) * (B)) && MODE != XM_PSI;                                          \
-        auto kfn = &k_xtile<MODE, SV, A, B, TK, NP, TRv, PFv, FMv>;                                       \
+        auto kfn = &k_xtile<MODE, SV, A, B, TK, NP, TRv, PFv>;                                            \
         SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                    int(lds)));                                                            \
         if constexpr (PFv) {   /* persistent: the resident blocks stride over the tiles */              \
             static const int per_cu = [&] {                                                               \
                 int n = 1;                                                                                \
                 SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kfn), \
-                                                                    xt_threads(NP, TRv), lds));                      \
+                                                                    NP * TRv, lds));                      \
                 return std::max(1, n);                                                                    \
             }();                                                                                          \
             grid = unsigned(std::min<int64_t>(grid, int64_t(256) * per_cu));                              \
         }                                                                                                 \
-        hipLaunchKernelGGL(kfn, dim3(grid), dim3(xt_threads(NP, TRv)), lds, s, b);                                   \
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(NP * TRv), lds, s, b);                                   \
         done = true;                                                                                      \
     }
 #define SD_XT_S(A, B) \

@@ -8,12 +8,12 @@ export TMPDIR=/tmp
 O=gpurun_out/r5f
 mkdir -p $O
 T="python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-default-mode"
-for v in main pfq trx trxq; do
+for v in main pfq trx trxq coltrx trxall; do
   if [ $v = main ]; then L=""; else L=$PWD/exp/libspimdecon_$v.so; fi
   SPIMDECON_LIB=$L timeout -k 10 300 $T --c5-rank > $O/c5_$v.log 2>&1 || exit 1
   tail -1 $O/c5_$v.log > $O/c5_$v.json
 done
-for v in main qpf64 pipe1 pipe2 trx trxq; do
+for v in main qpf64 pipe1 pipe2 trx trxq coltrx trxall; do
   if [ $v = main ]; then L=""; else L=$PWD/exp/libspimdecon_$v.so; fi
   SPIMDECON_LIB=$L timeout -k 10 300 $T --strong > $O/c3_$v.log 2>&1 || exit 2
   tail -1 $O/c3_$v.log > $O/c3_$v.json
@@ -21,14 +21,11 @@ done
 python3 tools/ab_summary.py $O/c5_*.json $O/c3_*.json
 timeout -k 10 200 python3 -u bench.py --steps 10 --no-cpu-baseline --no-strong-line > $O/b540.log 2>&1 || exit 3
 tail -1 $O/b540.log > $O/b540.json
+SPIMDECON_LIB=$PWD/exp/libspimdecon_pf540.so timeout -k 10 200 python3 -u bench.py --steps 10 --no-cpu-baseline --no-strong-line > $O/b540_pf540.log 2>&1 || exit 3
+tail -1 $O/b540_pf540.log > $O/b540_pf540.json
 timeout -k 10 300 python3 -u bench.py --strong --local-slabs 8 --steps 3 --warmup 1 --no-cpu-baseline --no-default-mode > $O/c3x8.log 2>&1 || exit 4
 tail -1 $O/c3x8.log > $O/c3x8.json
-python3 tools/ab_summary.py $O/b540.json $O/c3x8.json
-B="python3 -u bench.py --steps 1 --warmup 1 --no-timing --no-cpu-baseline --no-default-mode --no-strong-line"
-S=$PWD/exp/libspimdecon_stamp.so
-SPIMDECON_LIB=$S timeout -k 10 200 $B > $O/s540.log 2>&1 || exit 6
-SPIMDECON_LIB=$S timeout -k 10 300 $B --c5-rank > $O/s2100.log 2>&1 || exit 7
-for f in s540 s2100; do echo "== $f"; grep xt_stamp $O/$f.log | grep -v tiles=0 | tail -2; done
-timeout -k 10 700 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_rl.py tests/test_gpu_multidevice.py tests/test_gpu_configs.py -k "c5_rank or c5_decomposition or tikhonov or fp16 or split or slab or c3_" -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1
+python3 tools/ab_summary.py $O/b540.json $O/b540_pf540.json $O/c3x8.json
+timeout -k 10 700 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_rl.py tests/test_gpu_multidevice.py tests/test_gpu_configs.py -k "c5_rank or c5_decomposition or tikhonov or y_split or c3_decomposition or device_groups" -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit 5
 echo done-f
