@@ -263,10 +263,9 @@ int mvd_fft_dims(mvd_session* h, int slab, int64_t* out3);
  * keeps compact kernels (the z pass builds their z transform), else Mz */
 int mvd_kernel_planes(mvd_session* h, int slab, int* planes);
 /* z pass of the engine (info/bench): 0 = fused FFT z pass with full kernel
- * spectra, 1 = fused FFT z pass with compact kernels, 2 = direct circular
- * convolution with the compact kernel (only the nz interior planes written),
- * 3 = the same over z chunks carried inside a block, 4 = the fused y-z-y pass (y
- * transforms and the direct z convolution in one pass over kx-major spectra);
+ * spectra, 1 = fused FFT z pass with compact kernels, 3 = direct circular
+ * convolution with the compact kernel over z chunks carried inside a block (only
+ * the nz interior planes written; 2 and 4 named passes removed in round 5);
  * -1 for the rocFFT backend */
 int mvd_zpass_mode(mvd_session* h, int slab, int* mode);
 /* x pass of the last update launch of slab s (info/tests): 2 = two-factor row-pair

@@ -273,7 +273,7 @@ class Session:
         return out.value
 
     def zpass_mode(self, slab=0):
-        """0 fused FFT z pass (full kernels), 1 fused FFT (compact), 2 direct z convolution."""
+        """0 fused FFT z pass (full kernels), 1 fused FFT (compact), 3 direct z convolution (z chunks)."""
         out = C.c_int()
         check(self.lib.mvd_zpass_mode(self.h, int(slab), C.byref(out)))
         return out.value
