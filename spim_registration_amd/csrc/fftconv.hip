@@ -669,12 +669,9 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
     // blocks per CU: 128-B segments won at 800 (C4 RL 815 -> 745 ms per timepoint)
     const size_t budget = size_t(160) * 1024;
     auto tile_lds = [&](int tx) { return size_t(L * tx + L + (MODE == 5 ? f.n2 * tx : 0)) * sizeof(float2); };
-    // (-DSD_COL_TX8_MIN=n, A/B builds: 8-column tiles from length n at 64 threads per
-    // column -- two blocks per CU instead of one at 1050)
-#ifndef SD_COL_TX8_MIN
-#define SD_COL_TX8_MIN 1 << 30
-#endif
-    const int TX = tile_lds(k2fTX) <= budget && !(tr == 64 && L >= (SD_COL_TX8_MIN)) ? k2fTX : 8;
+    // (1050, 64 threads per column: 8-column tiles at two blocks per CU measured slower,
+    // y pass 0.892 -> 1.098 ms, profiles/r05_ypass_tx8_ab.txt)
+    const int TX = tile_lds(k2fTX) <= budget ? k2fTX : 8;
     const int kplanes = MODE == 5 ? 2 * kc + 1 : 0;
     const size_t lds = tile_lds(TX);
     const uint64_t bytes = uint64_t(p.spectrum_elems()) * sizeof(float2);

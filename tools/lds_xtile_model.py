@@ -9,6 +9,7 @@ the three modes, to compare with SQ_LDS_BANK_CONFLICT / SQ_WAVES of the PMC summ
 
 usage: python tools/lds_xtile_model.py [N1 N2 nx] [--swap] [--remap]
   --remap: also the DFT-phase lane map AM = 2 (xt_amap in fftconv_xt.inc) over pitches L+2..L+16
+  --np=N: N row pairs per tile (default 8); --pitches: the update tile over pitches L+2..L+16
 """
 import sys
 from collections import defaultdict
@@ -74,7 +75,11 @@ def model(N1, N2, nx, mode, swap=False, NP=8, TR=32, cx=None, P=None, amap=0):
             cl = {}
             for l in lanes:
                 t = w * 64 + l
-                cl[l] = ((t >> amap) & (NP - 1), (t & ((1 << amap) - 1)) | ((t >> (amap + lnp)) << amap))
+                if NP & (NP - 1):   # NP not a power of two: amap low bits r, then c = u % NP, r_hi = u / NP
+                    u = t >> amap
+                    cl[l] = (u % NP, (t & ((1 << amap) - 1)) | ((u // NP) << amap))
+                else:
+                    cl[l] = ((t >> amap) & (NP - 1), (t & ((1 << amap) - 1)) | ((t >> (amap + lnp)) << amap))
             for n1 in range(N1):
                 a = {l: zaddr(c, N2 * n1 + r) for l, (c, r) in cl.items() if r < N2}
                 if a:
@@ -166,10 +171,16 @@ if __name__ == "__main__":
     TR = 64 if max(N1, N2) > 32 else 32
     L = N1 * N2
     P0 = L + 2 + (2 if (L + 2) % 4 == 0 else 0)
+    NP = next((int(a[5:]) for a in sys.argv if a.startswith("--np=")), 8)
     for mode in ("psi", "quot", "update"):
-        r = model(N1, N2, nx, mode, swap="--swap" in sys.argv, TR=TR, P=P0)
+        r = model(N1, N2, nx, mode, swap="--swap" in sys.argv, TR=TR, P=P0, NP=NP)
         print(f"{mode:7s} total {sum(r.values()):7.1f} per wave:  " +
               ", ".join(f"{k} {v:.1f}" for k, v in sorted(r.items()) if v))
+    if "--pitches" in sys.argv:
+        for P in range(L + 2, L + 18, 2):
+            print(f"NP={NP} pitch L+{P - L:<2d} update total " + " ".join(
+                f"AM={am}: {sum(model(N1, N2, nx, 'update', swap=True, TR=TR, P=P, NP=NP, amap=am).values()):7.1f}"
+                for am in range(4)))
     if "--remap" in sys.argv:
         for P in range(L + 2, L + 18, 2):
             r = model(N1, N2, nx, "update", swap=True, TR=TR, P=P, amap=2)

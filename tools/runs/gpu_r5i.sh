@@ -1,0 +1,23 @@
+#!/bin/bash
+# round 5 (i): fftconv.hip compiled without machine LICM (nolicm: no hoisted DFT constants
+# spilling SGPRs in the persistent 2100 x tiles and the tile-looping column passes) vs main;
+# C5 rank, 540 headline, C3, C4; alternated twice on one box
+export TMPDIR=/tmp
+O=gpurun_out/r5i
+mkdir -p $O
+T="python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-default-mode"
+for k in 1 2; do
+for v in main nolicm; do
+  if [ $v = main ]; then L=""; else L=$PWD/exp/libspimdecon_$v.so; fi
+  SPIMDECON_LIB=$L timeout -k 10 300 $T --c5-rank > $O/c5_${v}_$k.log 2>&1 || exit 1
+  tail -1 $O/c5_${v}_$k.log > $O/c5_${v}_$k.json
+  SPIMDECON_LIB=$L timeout -k 10 200 python3 -u bench.py --steps 10 --no-cpu-baseline --no-strong-line > $O/b540_${v}_$k.log 2>&1 || exit 2
+  tail -1 $O/b540_${v}_$k.log > $O/b540_${v}_$k.json
+  SPIMDECON_LIB=$L timeout -k 10 300 $T --strong > $O/c3_${v}_$k.log 2>&1 || exit 3
+  tail -1 $O/c3_${v}_$k.log > $O/c3_${v}_$k.json
+  SPIMDECON_LIB=$L timeout -k 10 300 $T --size 768 --views 8 --ksize 31 --psftype OPTIMIZATION_I --lam 0.006 --no-strong-line > $O/c4_${v}_$k.log 2>&1 || exit 4
+  tail -1 $O/c4_${v}_$k.log > $O/c4_${v}_$k.json
+done
+done
+python3 tools/ab_summary.py $O/c5_*.json $O/b540_*.json $O/c3_*.json $O/c4_*.json
+echo done-i
