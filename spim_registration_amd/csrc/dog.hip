@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -429,24 +430,35 @@ __device__ __forceinline__ DzBox xcd_box(bool xcd) {
     return {int(l % gx), int((l / gx) % gy), int(l / (gx * gy))};
 }
 
+// Strips: a block walks one 64-column strip of one plane down y in steps of TY output rows.
+// Each step stages, normalises and x-convolves only its TY new input rows; the KW - 1 rows
+// above them are the previous step's last x results, carried (the y phase's last run holds
+// them in registers and writes them to the first LDS rows after a barrier), and a strip
+// starts with the KW - 1 rows above its first step.  Tiles of TY rows (round 4) recomputed
+// the KW - 1 halo rows of every tile: (TY + KW - 1) / TY = 1.29 times the x phase and the
+// normalisation at TY = 48, against (ny + KW - 1) / ny = 1.02 here.  TY = 32: a step's x
+// phase is 32 rows x 8 segments = one item per thread (48 rows left two of the four waves
+// a second item, and the blocks of a CU run their phases in step, so the SIMDs of those
+// waves set the pace: no gain at 48), 4 blocks per CU; 768^3: k_dog_xy 1.63 -> 1.47 ms,
+// DoG 3.67 -> 3.52 ms (profiles/r05_dog_strips_ab.txt).
 template <int KW, int TY, bool BUF = true>
-__global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
+__global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
                                                 const float* __restrict__ mm, int xcd, int mm_exact) {
     constexpr int R = KW / 2;
     constexpr int IW = kDxyTX + KW - 1;          // staged input columns
     constexpr int IP = dxy_in_pitch(IW);         // pitch (see dxy_in_pitch)
-    constexpr int IH = TY + KW - 1;              // staged input rows
-    constexpr int IHP = (IH + 63) / 64 * 64;     // x phase: rows padded to whole waves
+    constexpr int IH = TY + KW - 1;              // x-result rows of a step's window
     constexpr int NSEG = kDxyTX / kDxySeg;
     constexpr int WX = kDxySeg + KW - 1;
     constexpr int OY = TY / 4;                   // y outputs per thread (4 runs per column)
     constexpr int WY = OY + KW - 1;
-    __shared__ __attribute__((aligned(16))) float sin_[IH * IP];
+    static_assert(TY % 4 == 0 && OY + 2 * R == WY, "4 runs per column");
+    __shared__ __attribute__((aligned(16))) float sin_[TY * IP];
     __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxySxP];
     const int nx = int(d.nx), ny = int(d.ny);
     const int gx = (nx + kDxyTX - 1) / kDxyTX, gy = (ny + TY - 1) / TY;
-    const int ntiles = gx * gy * int(d.nz);
+    const int nstrips = gx * int(d.nz);
     const int t = threadIdx.x;
     // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
     bool norm = false;
@@ -466,48 +478,46 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
     const bool allfast = norm && mm_exact != 0 && rd != 0.0f && fabsf(mn) >= 0x1p-20f;
     // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
     // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
-    // load.  Tiles whose staged box lies inside the volume (all but the outer ring of
-    // tiles) index without the mirror arithmetic.
+    // load.  Steps whose staged box lies inside the volume index without the mirror
+    // arithmetic.
     constexpr int RPT = 256 / IW;                // rows staged per pass
     constexpr int IPC = 256 / RPT;               // threads per row (>= IW)
-    constexpr int NE = (IH + RPT - 1) / RPT;     // rows per thread
+    constexpr int NE = (TY + RPT - 1) / RPT;     // rows per thread and step
     const int col = t % IPC, r0 = t / IPC;
     const bool cact = col < IW && r0 < RPT;
-    auto tile_xyz = [&](int tile, int& x0, int& y0, uint32_t& plane) {   // x fastest, then y, then z
-        x0 = (tile % gx) * kDxyTX;
-        y0 = ((tile / gx) % gy) * TY;
-        plane = uint32_t(tile / (gx * gy)) * uint32_t(ny) * uint32_t(nx);
-    };
     // BUF (image below 4 GiB): buffer loads, the lane's row offset in a VGPR and the
     // pass offset RPT * e * nx in the scalar offset (no per-load address arithmetic; rows
-    // past the tile load in range or return 0 and are never staged); y mirror indices by
+    // past the step load in range or return 0 and are never staged); y mirror indices by
     // one reflection when ny > R (the modulo of mirror32 cost ~15 VALU per staged value
-    // on the border tiles)
+    // on the border strips)
     const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(in), 0, int(uint32_t(BUF ? uint64_t(d.nx * d.ny * d.nz) * 4u : 0u)), 0x00020000);
     const bool yrefl = ny > R;
-    auto stage_loads = [&](int tile, float* v) {
-        int x0, y0;
-        uint32_t plane;
-        tile_xyz(tile, x0, y0, plane);
-        const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && y0 - R >= 0 && y0 - R + IH <= ny;
+    // input rows [ys, ys + NR) of strip s -> v (row r0 + RPT e of the unit; NR = 2R for the
+    // rows above a strip, TY for a step)
+    auto stage_loads = [&](int s, int ys, auto nrc, float* v) {
+        constexpr int NR = decltype(nrc)::value;
+        constexpr int NEc = (NR + RPT - 1) / RPT;
+        const int x0 = (s % gx) * kDxyTX;
+        const uint32_t plane = uint32_t(s / gx) * uint32_t(ny) * uint32_t(nx);
+        const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && ys >= 0 && ys + NR <= ny;
         if (inside) {
-            const uint32_t base = plane + uint32_t(y0 - R) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
+            const uint32_t base = plane + uint32_t(ys) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
             if constexpr (BUF) {
                 const uint32_t vo = (base + uint32_t(r0) * uint32_t(nx)) * 4u;
 #pragma unroll
-                for (int e = 0; e < NE; ++e)
+                for (int e = 0; e < NEc; ++e)
                     v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                          rin, int(vo), int(uint32_t(RPT * e) * uint32_t(nx) * 4u), 0));
             } else {
 #pragma unroll
-                for (int e = 0; e < NE; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, IH - 1)) * uint32_t(nx)];
+                for (int e = 0; e < NEc; ++e) v[e] = in[base + uint32_t(min(r0 + RPT * e, NR - 1)) * uint32_t(nx)];
             }
         } else {
             const uint32_t gxo = plane + uint32_t(mirror32(x0 - R + min(col, IW - 1), nx));
 #pragma unroll
-            for (int e = 0; e < NE; ++e) {
-                const int yy = y0 - R + min(r0 + RPT * e, IH - 1);
+            for (int e = 0; e < NEc; ++e) {
+                const int yy = ys + min(r0 + RPT * e, NR - 1);
                 const int my = yrefl ? (ny - 1) - abs((ny - 1) - abs(yy)) : mirror32(yy, ny);
                 if constexpr (BUF)
                     v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -517,28 +527,16 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
             }
         }
     };
-    // persistent blocks: the next tile's input values are loaded into registers while
-    // this tile is transformed (one tile per block exposed the HBM latency of staging)
-    // xcd: blocks go round-robin to the 8 XCDs (each its own L2); the logical block index
-    // makes XCD k's blocks a contiguous range, so the tiles one XCD holds at a time are x
-    // and y neighbours whose halo lines its L2 serves (else they come from HBM twice)
-    float v[NE];
-    int tile = int(blockIdx.x);
-    if (xcd) {
-        const unsigned b = blockIdx.x, k = b & 7u, j = b >> 3, q = gridDim.x >> 3, r = gridDim.x & 7u;
-        tile = int(k * q + min(k, r) + j);
-    }
-    if (tile < ntiles) stage_loads(tile, v);
-    for (; tile < ntiles; tile += gridDim.x) {
-        int x0, y0;
-        uint32_t plane;
-        tile_xyz(tile, x0, y0, plane);
+    // normalise the staged values of a step and store them to the LDS rows
+    auto norm_store = [&](auto nrc, float* v) {
+        constexpr int NR = decltype(nrc)::value;
+        constexpr int NEc = (NR + RPT - 1) / RPT;
         if (norm) {
-            // one wave-uniform decision for all NE values: the reciprocal path unless a
-            // value of the wave leaves its exact range (then the IEEE division for all)
+            // one wave-uniform decision for all values: the reciprocal path unless a value
+            // of the wave leaves its exact range (then the IEEE division for all)
             bool bad = rd == 0.0f;
 #pragma unroll
-            for (int e = 0; e < NE; ++e) {
+            for (int e = 0; e < NEc; ++e) {
                 v[e] = __fsub_rn(v[e], mn);
                 if (!allfast) {
                     const float aa = fabsf(v[e]);
@@ -547,28 +545,28 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
             }
             if (allfast || !__any(bad)) {
 #pragma unroll
-                for (int e = 0; e < NE; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
+                for (int e = 0; e < NEc; ++e) v[e] = div_rn_rcp_core(v[e], diff, rd);
             } else {
 #pragma unroll
-                for (int e = 0; e < NE; ++e) v[e] = __fdiv_rn(v[e], diff);
+                for (int e = 0; e < NEc; ++e) v[e] = __fdiv_rn(v[e], diff);
             }
         }
-        if (cact) {   // (the previous tile's x phase finished at its mid-tile barrier)
+        if (cact) {   // (the previous step's x phase finished at its mid-step barrier)
 #pragma unroll
-            for (int e = 0; e < NE; ++e) {
+            for (int e = 0; e < NEc; ++e) {
                 const int row = r0 + RPT * e;
-                if (row >= IH) break;
+                if (row >= NR) break;
                 sin_[row * IP + col] = v[e];
             }
         }
-        const int next = tile + int(gridDim.x);
-        if (next < ntiles) stage_loads(next, v);   // in flight during this tile's phases
-        __syncthreads();   // (also: the previous tile's y phase no longer reads sx)
-        // x phase: lane = staged row, the wave's segment of kDxySeg outputs from a window
-        // of WX values (b128 reads conflict-free through the pitch IP)
-        for (int it = t; it < IHP * NSEG; it += 256) {
-            const int row = it % IHP, seg = it / IHP;
-            if (row >= IH) continue;
+    };
+    // x phase over the step's NR staged rows into sx rows xrow0 + row: lane = staged row,
+    // a segment of kDxySeg outputs from a window of WX values (b128 reads through the pitch IP)
+    auto x_phase = [&](auto nrc, int xrow0) {
+        constexpr int NR = decltype(nrc)::value;
+#pragma unroll 1
+        for (int it = t; it < NR * NSEG; it += 256) {
+            const int row = it % NR, seg = it / NR;
             const float* src = sin_ + row * IP + seg * kDxySeg;
             float w[WX];
 #pragma unroll
@@ -582,16 +580,60 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
 #pragma unroll
                 for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
             }
-            float2* dst = sx + row * kDxySxP + seg * kDxySeg;
+            float2* dst = sx + (xrow0 + row) * kDxySxP + seg * kDxySeg;
 #pragma unroll
             for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
         }
+    };
+    using PREc = std::integral_constant<int, 2 * R>;
+    using TYc = std::integral_constant<int, TY>;
+    // persistent blocks over the strips; the next step's input values are loaded into
+    // registers while this step is transformed
+    // xcd: blocks go round-robin to the 8 XCDs (each its own L2); the logical block index
+    // makes XCD k's blocks a contiguous range, so the strips one XCD holds at a time are x
+    // neighbours whose halo columns its L2 serves (else they come from HBM twice)
+    float v[NE];
+    int strip = int(blockIdx.x);
+    if (xcd) {
+        const unsigned b = blockIdx.x, k = b & 7u, j = b >> 3, q = gridDim.x >> 3, r = gridDim.x & 7u;
+        strip = int(k * q + min(k, r) + j);
+    }
+    // units of a strip: step -1 stages and x-convolves the 2R rows above the strip into sx
+    // rows 0 .. 2R - 1; step k >= 0 its TY new rows [k TY + R, k TY + TY + R) into sx rows
+    // 2R .., then the y phase of output rows [k TY, k TY + TY)
+    int step = -1;
+    if (strip < nstrips) stage_loads(strip, -R, PREc{}, v);
+    const int c = t & (kDxyTX - 1), run = t / kDxyTX;
+    while (strip < nstrips) {
+        const int x0 = (strip % gx) * kDxyTX;
+        const uint32_t plane = uint32_t(strip / gx) * uint32_t(ny) * uint32_t(nx);
+        const int y0 = step * TY;
+        const bool pre = step < 0;
+        if (pre) norm_store(PREc{}, v);
+        else norm_store(TYc{}, v);
+        // the next unit's values are in flight during this unit's phases
+        int nstrip = strip, nstep = step + 1;
+        if (nstep == gy) {
+            nstrip = strip + int(gridDim.x);
+            nstep = -1;
+        }
+        if (nstrip < nstrips) {
+            if (nstep < 0) stage_loads(nstrip, -R, PREc{}, v);
+            else stage_loads(nstrip, nstep * TY + R, TYc{}, v);
+        }
+        __syncthreads();   // (also: the previous step's y phase no longer reads sx)
+        if (pre) x_phase(PREc{}, 0);
+        else x_phase(TYc{}, 2 * R);
         __syncthreads();
+        if (pre) {   // (block-uniform)
+            strip = nstrip;
+            step = nstep;
+            continue;
+        }
         // y phase: column c, OY consecutive outputs
-        const int c = t & (kDxyTX - 1), run = t / kDxyTX;
         const int x = x0 + c;
+        dg_v2 w[WY];
         if (x < nx) {
-            dg_v2 w[WY];
 #pragma unroll
             for (int i = 0; i < WY; ++i) {
                 const float2 vv = sx[(run * OY + i) * kDxySxP + c];
@@ -612,6 +654,17 @@ __global__ __launch_bounds__(256) void k_dog_xy(Dims3 d, const float* __restrict
                 if (y < ny) g12[plane + uint32_t(y) * uint32_t(nx) + uint32_t(x)] = make_float2(acc[o].x, acc[o].y);
             }
         }
+        // the last run holds the x results of the next step's first 2R rows: to sx rows
+        // 0 .. 2R - 1 once every run has read its window (block-uniform branch)
+        if (nstep >= 0) {
+            __syncthreads();
+            if (run == 3 && x < nx) {
+#pragma unroll
+                for (int i = 0; i < 2 * R; ++i) sx[i * kDxySxP + c] = make_float2(w[OY + i].x, w[OY + i].y);
+            }
+        }
+        strip = nstrip;
+        step = nstep;
     }
 }
 
@@ -1710,12 +1763,13 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
                        d.nz <= 65535;
     // (chunk + 2 + KW - 1 source planes must fit k_dog_z's kDzMaxLen plane table)
     const int zc = std::min(kDzMaxLen - 128, kDzChunk);
-    constexpr int ty = 48;     // (48-row tiles: 32 measured slower)
+    constexpr int ty = 32;     // strip steps (48-row tiles: 32 measured slower; strips: 32 beat 48, r05_dog_strips_ab.txt)
     constexpr int xcd = 1;     // XCD-contiguous y-fastest boxes of k_dog_z
     constexpr int xcd_xy = 1;  // XCD-contiguous tile ranges of k_dog_xy
-    // k_dog_xy: persistent blocks (3 per CU: 53.6 KB of LDS each, 16 rounds of them), tiles x fastest
-    const int64_t xy_tiles = ceil_div(d.nx, kDxyTX) * ceil_div(d.ny, ty) * d.nz;
-    const dim3 gxy(unsigned(std::min<int64_t>(xy_tiles, int64_t(256) * 3 * 16)));
+    // k_dog_xy: persistent blocks (4 per CU at 32-row steps: 34.5 KB of LDS each), strips x
+    // fastest
+    const int64_t xy_strips = ceil_div(d.nx, kDxyTX) * d.nz;
+    const dim3 gxy(unsigned(std::min<int64_t>(xy_strips, int64_t(256) * 4)));
     // k_dog_z box: 64 x 8 (512 threads); 64 x 16 and 32 x 16 measured slower (r3i)
     constexpr int bx = 64, bz_y = 8;
     // scalar plane indices (one mirror reflection: nz > K / 2; plane bytes in 31 bits)
