@@ -3,7 +3,7 @@
 # line, its kernel trace and PMC passes, the C3 / C4 / C5-rank class lines, the C3 8-slab
 # exchange window and the C4 pipeline
 export TMPDIR=/tmp
-O=gpurun_out/r5z
+O=${O:-gpurun_out/r5z}
 mkdir -p $O
 if [ "$1" != "meas" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rA --durations=20 --timeout 600 --timeout-method thread > $O/tests.log 2>&1
