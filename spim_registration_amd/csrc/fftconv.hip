@@ -519,16 +519,16 @@ bool x_buffer_args(const XArgs& a, Store st, const SpectralPlan& p, XArgs& b) {
 }
 
 // k_xtile for two-factor lengths; returns the grid, 0 when it does not apply.
-// 8 row pairs per tile, one tile per block: fresh blocks keep loading while the resident
+// xt_np row pairs per tile, one tile per block: fresh blocks keep loading while the resident
 // ones transform (quotient 0.40 vs 0.43 ms with 16 pairs and 0.45 with 4, update 0.52 vs
 // 0.58 / 0.54 ms at 540; at L = 1050 quotient 0.90 vs 1.05 ms with 16 pairs; grid-stride
 // blocks in lock step measured slower)
 template <int MODE>
 unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream_t s) {
-    constexpr int NP = 8;
     XArgs b;
     if (!p.fx.n1 || !x_buffer_args(a, st, p, b)) return 0;
     const int L = int(p.g.Mx);
+    const int NP = xt_np(MODE, L);
     const size_t lds = xt_lds(L, NP, xt_twg(L, NP));
     if (lds > 160 * 1024) return 0;
     unsigned grid = unsigned(std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(NP))));
@@ -539,19 +539,20 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                               \
         constexpr int TRv = SD_2F_TR(A, B);                                                               \
         constexpr bool PFv = xt_pf((A) * (B)) && MODE != XM_PSI;                                          \
-        auto kfn = &k_xtile<MODE, SV, A, B, TK, NP, TRv, PFv>;                                            \
+        constexpr int NPv = xt_np(MODE, (A) * (B));                                                       \
+        auto kfn = &k_xtile<MODE, SV, A, B, TK, NPv, TRv, PFv>;                                           \
         SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                    int(lds)));                                                            \
         if constexpr (PFv) {   /* persistent: the resident blocks stride over the tiles */              \
             static const int per_cu = [&] {                                                               \
                 int n = 1;                                                                                \
                 SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kfn), \
-                                                                    NP * TRv, lds));                      \
+                                                                    NPv * TRv, lds));                     \
                 return std::max(1, n);                                                                    \
             }();                                                                                          \
             grid = unsigned(std::min<int64_t>(grid, int64_t(256) * per_cu));                              \
         }                                                                                                 \
-        hipLaunchKernelGGL(kfn, dim3(grid), dim3(NP * TRv), lds, s, b);                                   \
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(NPv * TRv), lds, s, b);                                  \
         done = true;                                                                                      \
     }
 #define SD_XT_S(A, B) \
