@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include <memory>
@@ -37,16 +39,21 @@ struct Dim3 {
 // chunk in parallel, then each voxel's float sum over the chunk in bead order (the
 // reference's order, so the result is bit-identical to the one-thread-per-voxel loop,
 // which left all but a few dozen CUs idle: 57 ms for 67k beads of a 768^3 view).
+// grid (voxel blocks, beads): the bead from blockIdx.y and 32-bit voxel coordinates (the
+// flat 64-bit index's divisions were ~100-instruction software routines per division)
 __global__ __launch_bounds__(kPsfBlock) void k_psf_samples(const float* __restrict__ img, Dim3 s,
                                                            const double* __restrict__ locs, int64_t nb, Dim3 p,
                                                            float* __restrict__ samp) {
-    const int64_t np = p.n();
-    const int64_t k = int64_t(blockIdx.x) * kPsfBlock + threadIdx.x;
-    if (k >= nb * np) return;
-    const int64_t l = k / np, i = k - l * np;
-    const int x = int(i % p.x), y = int((i / p.x) % p.y), z = int(i / (int64_t(p.x) * p.y));
-    samp[k] = nlinear_at<kExtPeriodic>(img, s.x, s.y, s.z, double(x - p.x / 2) + locs[3 * l],
-                                       double(y - p.y / 2) + locs[3 * l + 1], double(z - p.z / 2) + locs[3 * l + 2]);
+    const uint32_t np = uint32_t(p.n());
+    const uint32_t i = blockIdx.x * kPsfBlock + threadIdx.x;
+    const uint32_t l = blockIdx.y;
+    if (i >= np || int64_t(l) >= nb) return;
+    const uint32_t px = uint32_t(p.x), pxy = uint32_t(p.x) * uint32_t(p.y);
+    const int z = int(i / pxy), r = int(i - uint32_t(z) * pxy);
+    const int y = r / int(px), x = r - y * int(px);
+    samp[int64_t(l) * np + i] = nlinear_at<kExtPeriodic>(img, s.x, s.y, s.z, double(x - p.x / 2) + locs[3 * l],
+                                                         double(y - p.y / 2) + locs[3 * l + 1],
+                                                         double(z - p.z / 2) + locs[3 * l + 2]);
 }
 
 __global__ __launch_bounds__(kPsfBlock) void k_psf_accumulate(const float* __restrict__ samp, int64_t nb,
@@ -55,12 +62,15 @@ __global__ __launch_bounds__(kPsfBlock) void k_psf_accumulate(const float* __res
     if (i >= np) return;
     float a = acc[i];
     int64_t l = 0;
-    for (; l + 8 <= nb; l += 8) {   // loads ahead, adds in bead order
-        float v[8];
+    // 32 loads ahead, adds in bead order (with 8 the ~9k chains of a view waited on one HBM
+    // round trip per 8 beads)
+    constexpr int U = 32;
+    for (; l + U <= nb; l += U) {
+        float v[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = samp[(l + u) * np + i];
+        for (int u = 0; u < U; ++u) v[u] = samp[(l + u) * np + i];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a = a + v[u];
+        for (int u = 0; u < U; ++u) a = a + v[u];
     }
     for (; l < nb; ++l) a = a + samp[l * np + i];
     acc[i] = a;
@@ -251,6 +261,34 @@ void transform_psf(const float* psf, const int64_t* psf_size, const double* mode
     SD_HIP(hipStreamSynchronize(st.s));
 }
 
+namespace {
+// One view's device buffers and stream, kept across calls (per device; the pool is never
+// destroyed: no destructor racing the HIP runtime's teardown at exit).  Fresh buffers and
+// streams per call cost a hipMalloc / hipFree (which synchronises the device) per buffer
+// and view: the C4 pipeline's PSF stage spent most of its time there.
+struct PsfWork {
+    Stream st;
+    DBuf<float> dimg, dpsf, samp, dt;
+    DBuf<double> dloc, mm;
+};
+template <typename T>
+void ensure(DBuf<T>& b, size_t n) {
+    if (b.n < n) b.alloc(n);
+}
+struct PsfPool {
+    std::mutex mu;   // one extract call at a time per device
+    std::vector<std::unique_ptr<PsfWork>> w;
+};
+std::mutex g_psf_pool_mu;
+std::map<int, std::unique_ptr<PsfPool>>& g_psf_pool = *new std::map<int, std::unique_ptr<PsfPool>>();
+PsfPool& psf_pool(int dev) {
+    std::lock_guard<std::mutex> lk(g_psf_pool_mu);
+    auto& p = g_psf_pool[dev];
+    if (!p) p.reset(new PsfPool());
+    return *p;
+}
+}  // namespace
+
 // One view's ExtractPSF.extract (:281-299) + transformPSF, in three steps so several
 // views can run concurrently (extract_psfs): the per-voxel sum over the beads is a
 // serial float chain in bead order (bit-exact with the reference), so one view offers
@@ -263,74 +301,76 @@ struct PsfJob {
     float* psf_original = nullptr;
     float* psf_transformed = nullptr;
     int64_t psf_size[3] = {0, 0, 0};
-    Stream st;
-    DBuf<float> dimg, dpsf, samp, dt;
-    DBuf<double> dloc, mm;
+    PsfWork& w;
     const float* src = nullptr;
     int64_t chunk = 0;
+    int64_t tn = 0;   // transformed PSF voxels
 
-    PsfJob(const float* img_, const int64_t* dims, int img_on_device, const double* locations, int64_t nloc_,
-           const int64_t* psf_size_, const double* model_, float* orig, float* trans)
-        : img(img_), model(model_), nloc(nloc_), psf_original(orig), psf_transformed(trans) {
+    PsfJob(PsfWork& w_, const float* img_, const int64_t* dims, int img_on_device, const double* locations,
+           int64_t nloc_, const int64_t* psf_size_, const double* model_, float* orig, float* trans)
+        : img(img_), model(model_), nloc(nloc_), psf_original(orig), psf_transformed(trans), w(w_) {
         SD_CHECK(img && psf_original && nloc >= 0 && (nloc == 0 || locations), SPIMDECON_ERR_ARG, "null argument");
         SD_CHECK(!psf_transformed || model, SPIMDECON_ERR_ARG, "a transformed PSF needs the view model");
         s = dim3_of(dims, "image");
         p = dim3_of(psf_size_, "psf");
         std::memcpy(psf_size, psf_size_, sizeof(psf_size));
-        // allocations and uploads (asynchronous on this job's stream)
+        // buffers (grown, reused) and uploads (asynchronous on this job's stream)
         src = img;
         if (!img_on_device) {
-            dimg.alloc(s.n());
-            SD_HIP(hipMemcpyAsync(dimg.p, img, s.n() * 4, hipMemcpyHostToDevice, st.s));
-            src = dimg.p;
+            ensure(w.dimg, s.n());
+            SD_HIP(hipMemcpyAsync(w.dimg.p, img, s.n() * 4, hipMemcpyHostToDevice, w.st.s));
+            src = w.dimg.p;
         }
-        dloc.alloc(size_t(std::max<int64_t>(nloc, 1)) * 3);
-        if (nloc) SD_HIP(hipMemcpyAsync(dloc.p, locations, nloc * 24, hipMemcpyHostToDevice, st.s));
-        dpsf.alloc(p.n());
-        mm.alloc(2);
-        if (nloc > 64) {   // bead chunks of <= 2^26 samples (256 MB)
-            chunk = std::max<int64_t>(1, std::min<int64_t>(nloc, (int64_t(1) << 26) / p.n()));
-            samp.alloc(size_t(chunk * p.n()));
+        ensure(w.dloc, size_t(std::max<int64_t>(nloc, 1)) * 3);
+        if (nloc) SD_HIP(hipMemcpyAsync(w.dloc.p, locations, nloc * 24, hipMemcpyHostToDevice, w.st.s));
+        ensure(w.dpsf, p.n());
+        ensure(w.mm, 2);
+        if (nloc > 64) {   // bead chunks of <= 2^26 samples (256 MB), <= 65535 beads (grid.y)
+            SD_CHECK(p.n() < (int64_t(1) << 31), SPIMDECON_ERR_ARG, "psf too large");
+            chunk = std::max<int64_t>(1, std::min<int64_t>({nloc, (int64_t(1) << 26) / p.n(), int64_t(65535)}));
+            ensure(w.samp, size_t(chunk * p.n()));
         }
         if (psf_transformed) {
             int64_t ts[3];
             double off[3];
             transformed_size(psf_size, model, ts, off);
-            dt.alloc(dim3_of(ts, "transformed psf").n());
+            tn = dim3_of(ts, "transformed psf").n();
+            ensure(w.dt, size_t(tn));
         }
     }
 
     void launch() {
+        const hipStream_t st = w.st.s;
         if (nloc <= 64) {
-            hipLaunchKernelGGL(k_psf_extract, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, src, s, dloc.p, nloc,
-                               p, dpsf.p);
+            hipLaunchKernelGGL(k_psf_extract, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st, src, s, w.dloc.p, nloc,
+                               p, w.dpsf.p);
         } else {
-            SD_HIP(hipMemsetAsync(dpsf.p, 0, p.n() * 4, st.s));
+            SD_HIP(hipMemsetAsync(w.dpsf.p, 0, p.n() * 4, st));
             for (int64_t l0 = 0; l0 < nloc; l0 += chunk) {
                 const int64_t nb = std::min(chunk, nloc - l0);
-                hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(nb * p.n(), kPsfBlock))), dim3(kPsfBlock),
-                                   0, st.s, src, s, dloc.p + 3 * l0, nb, p, samp.p);
-                hipLaunchKernelGGL(k_psf_accumulate, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, samp.p, nb,
-                                   p.n(), dpsf.p);
+                hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(p.n(), kPsfBlock)), unsigned(nb)),
+                                   dim3(kPsfBlock), 0, st, src, s, w.dloc.p + 3 * l0, nb, p, w.samp.p);
+                hipLaunchKernelGGL(k_psf_accumulate, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st, w.samp.p, nb,
+                                   p.n(), w.dpsf.p);
             }
         }
         SD_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_psf_minmax, dim3(1), dim3(1024), 0, st.s, dpsf.p, p.n(), mm.p);
+        hipLaunchKernelGGL(k_psf_minmax, dim3(1), dim3(1024), 0, st, w.dpsf.p, p.n(), w.mm.p);
         SD_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st.s, dpsf.p, p.n(), mm.p);
+        hipLaunchKernelGGL(k_psf_normalize, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st, w.dpsf.p, p.n(), w.mm.p);
         SD_HIP(hipGetLastError());
         if (psf_transformed) {
             Dim3 t;
-            launch_transform(dpsf.p, p, model, dt.p, t, st.s);
+            launch_transform(w.dpsf.p, p, model, w.dt.p, t, st);
         }
     }
 
     // the copies out only now: a copy into pageable host memory blocks the host until
     // the stream has drained, which would serialise the views' launches
     void finish() {
-        SD_HIP(hipMemcpyAsync(psf_original, dpsf.p, p.n() * 4, hipMemcpyDefault, st.s));
-        if (psf_transformed) SD_HIP(hipMemcpyAsync(psf_transformed, dt.p, dt.n * 4, hipMemcpyDefault, st.s));
-        SD_HIP(hipStreamSynchronize(st.s));
+        SD_HIP(hipMemcpyAsync(psf_original, w.dpsf.p, p.n() * 4, hipMemcpyDefault, w.st.s));
+        if (psf_transformed) SD_HIP(hipMemcpyAsync(psf_transformed, w.dt.p, size_t(tn) * 4, hipMemcpyDefault, w.st.s));
+        SD_HIP(hipStreamSynchronize(w.st.s));
     }
 };
 
@@ -339,7 +379,10 @@ void extract_psf(const float* img, const int64_t* dims, int img_on_device, const
                  int device) {
     check_device(device);
     DeviceGuard guard(device);
-    PsfJob job(img, dims, img_on_device, locations, nloc, psf_size, model, psf_original, psf_transformed);
+    PsfPool& pool = psf_pool(device);
+    std::lock_guard<std::mutex> lk(pool.mu);
+    if (pool.w.empty()) pool.w.emplace_back(new PsfWork());
+    PsfJob job(*pool.w[0], img, dims, img_on_device, locations, nloc, psf_size, model, psf_original, psf_transformed);
     job.launch();
     job.finish();
 }
@@ -351,11 +394,14 @@ void extract_psfs(int nviews, const float* const* imgs, const int64_t* dims, int
              SPIMDECON_ERR_ARG, "null argument");
     check_device(device);
     DeviceGuard guard(device);
+    PsfPool& pool = psf_pool(device);
+    std::lock_guard<std::mutex> lk(pool.mu);
+    while (int(pool.w.size()) < nviews) pool.w.emplace_back(new PsfWork());
     std::vector<std::unique_ptr<PsfJob>> jobs;
     jobs.reserve(size_t(nviews));
     for (int v = 0; v < nviews; ++v)
-        jobs.emplace_back(new PsfJob(imgs[v], dims + 3 * v, img_on_device, locations[v], nlocations[v], psf_size,
-                                     models ? models + 12 * v : nullptr, psf_original[v],
+        jobs.emplace_back(new PsfJob(*pool.w[size_t(v)], imgs[v], dims + 3 * v, img_on_device, locations[v],
+                                     nlocations[v], psf_size, models ? models + 12 * v : nullptr, psf_original[v],
                                      psf_transformed ? psf_transformed[v] : nullptr));
     for (auto& j : jobs) j->launch();
     for (auto& j : jobs) j->finish();
