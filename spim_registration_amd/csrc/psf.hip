@@ -39,21 +39,57 @@ struct Dim3 {
 // chunk in parallel, then each voxel's float sum over the chunk in bead order (the
 // reference's order, so the result is bit-identical to the one-thread-per-voxel loop,
 // which left all but a few dozen CUs idle: 57 ms for 67k beads of a 768^3 view).
-// grid (voxel blocks, beads): the bead from blockIdx.y and 32-bit voxel coordinates (the
-// flat 64-bit index's divisions were ~100-instruction software routines per division)
+// grid (voxel blocks of kPsfSpt * kPsfBlock, beads): the bead from blockIdx.y, 32-bit voxel
+// coordinates (the flat 64-bit index's divisions were ~100-instruction software routines).
+// The sample at integer offset k from a bead at position c is the trilinear interpolation at
+// p = k + c (double).  Whenever that sum is exact -- always, unless |p| rises into the next
+// binade of |c| -- floor(p) = floor(c) + k and p - floor(p) = c - floor(c): the eight corner
+// weights are the bead's, computed once per thread for its kPsfSpt voxels; an inexact sum
+// (checked: (p - k) != c) takes nlinear_at itself.  The same operations on the same values
+// either way: bit-identical to nlinear_at per voxel.
+constexpr int kPsfSpt = 8;   // voxels per thread
 __global__ __launch_bounds__(kPsfBlock) void k_psf_samples(const float* __restrict__ img, Dim3 s,
                                                            const double* __restrict__ locs, int64_t nb, Dim3 p,
                                                            float* __restrict__ samp) {
     const uint32_t np = uint32_t(p.n());
-    const uint32_t i = blockIdx.x * kPsfBlock + threadIdx.x;
     const uint32_t l = blockIdx.y;
-    if (i >= np || int64_t(l) >= nb) return;
+    if (int64_t(l) >= nb) return;
+    const double c0 = locs[3 * l], c1 = locs[3 * l + 1], c2 = locs[3 * l + 2];
+    const double f0 = floor(c0), f1 = floor(c1), f2 = floor(c2);
+    const double w0 = c0 - f0, w1 = c1 - f1, w2 = c2 - f2;
+    const double i0 = 1.0 - w0, i1 = 1.0 - w1, i2 = 1.0 - w2;
+    // corner order of nlinear_at: 000, 100, 110, 010, 011, 111, 101, 001
+    const double W[8] = {i0 * i1 * i2, w0 * i1 * i2, w0 * w1 * i2, i0 * w1 * i2,
+                         i0 * w1 * w2, w0 * w1 * w2, w0 * i1 * w2, i0 * i1 * w2};
+    const int b0 = int(f0), b1 = int(f1), b2 = int(f2);
     const uint32_t px = uint32_t(p.x), pxy = uint32_t(p.x) * uint32_t(p.y);
-    const int z = int(i / pxy), r = int(i - uint32_t(z) * pxy);
-    const int y = r / int(px), x = r - y * int(px);
-    samp[int64_t(l) * np + i] = nlinear_at<kExtPeriodic>(img, s.x, s.y, s.z, double(x - p.x / 2) + locs[3 * l],
-                                                         double(y - p.y / 2) + locs[3 * l + 1],
-                                                         double(z - p.z / 2) + locs[3 * l + 2]);
+    const int64_t py = s.x, pz = int64_t(s.x) * s.y;
+    for (int v = 0; v < kPsfSpt; ++v) {
+        const uint32_t i = (blockIdx.x * kPsfSpt + uint32_t(v)) * kPsfBlock + threadIdx.x;
+        if (i >= np) break;
+        const int z = int(i / pxy), r = int(i - uint32_t(z) * pxy);
+        const int y = r / int(px), x = r - y * int(px);
+        const double k0 = double(x - p.x / 2), k1 = double(y - p.y / 2), k2 = double(z - p.z / 2);
+        const double q0 = k0 + c0, q1 = k1 + c1, q2 = k2 + c2;
+        const int xa = b0 + (x - p.x / 2), ya = b1 + (y - p.y / 2), za = b2 + (z - p.z / 2);
+        float out;
+        if (q0 - k0 == c0 && q1 - k1 == c1 && q2 - k2 == c2 && xa >= 0 && ya >= 0 && za >= 0 && xa + 1 < s.x &&
+            ya + 1 < s.y && za + 1 < s.z) {
+            const float* bp = img + (int64_t(za) * s.y + ya) * s.x + xa;
+            float acc = float(double(bp[0]) * W[0]);
+            acc = acc + float(double(bp[1]) * W[1]);
+            acc = acc + float(double(bp[py + 1]) * W[2]);
+            acc = acc + float(double(bp[py]) * W[3]);
+            acc = acc + float(double(bp[pz + py]) * W[4]);
+            acc = acc + float(double(bp[pz + py + 1]) * W[5]);
+            acc = acc + float(double(bp[pz + 1]) * W[6]);
+            acc = acc + float(double(bp[pz]) * W[7]);
+            out = acc;
+        } else {
+            out = nlinear_at<kExtPeriodic>(img, s.x, s.y, s.z, q0, q1, q2);
+        }
+        samp[int64_t(l) * np + i] = out;
+    }
 }
 
 __global__ __launch_bounds__(kPsfBlock) void k_psf_accumulate(const float* __restrict__ samp, int64_t nb,
@@ -348,7 +384,8 @@ struct PsfJob {
             SD_HIP(hipMemsetAsync(w.dpsf.p, 0, p.n() * 4, st));
             for (int64_t l0 = 0; l0 < nloc; l0 += chunk) {
                 const int64_t nb = std::min(chunk, nloc - l0);
-                hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(p.n(), kPsfBlock)), unsigned(nb)),
+                hipLaunchKernelGGL(k_psf_samples, dim3(unsigned(ceil_div(p.n(), int64_t(kPsfBlock) * kPsfSpt)),
+                                                       unsigned(nb)),
                                    dim3(kPsfBlock), 0, st, src, s, w.dloc.p + 3 * l0, nb, p, w.samp.p);
                 hipLaunchKernelGGL(k_psf_accumulate, dim3(grid_for(p.n())), dim3(kPsfBlock), 0, st, w.samp.p, nb,
                                    p.n(), w.dpsf.p);
