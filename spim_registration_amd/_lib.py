@@ -179,9 +179,10 @@ def load():
 
     torch wheels bundle their own libamdhip64.so.7; the loader keeps whichever
     copy of that soname comes first.  A process that uses torch on the GPU
-    together with this library must import torch before the first load() (as
-    bench.py and tests/test_gpu_psf.py do) so both share torch's HIP runtime;
-    the reverse order hands torch the /opt/rocm runtime and aborts at exit."""
+    together with this library must load torch's copy first so both share one
+    HIP runtime: the reverse order hands torch the /opt/rocm runtime, and the
+    process aborts at exit ("double free or corruption") after a torch GPU
+    call.  load() therefore imports torch (when installed) before the library."""
     global _lib
     if _lib is not None:
         return _lib
@@ -189,6 +190,10 @@ def load():
         raise RuntimeError(
             f"{LIB_PATH} not found: build it with `python -m spim_registration_amd.build` "
             "(there is no CPU fallback)")
+    try:
+        import torch  # noqa: F401  (binds the HIP runtime soname to torch's copy)
+    except ImportError:
+        pass
     lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)
