@@ -1,0 +1,256 @@
+"""Global optimisation of view models from point correspondences (host side).
+
+Restates the registration's last step, ``GlobalOpt.compute``
+(/root/reference/src/main/java/spim/process/interestpointregistration/GlobalOpt.java:44-135):
+one tile per view (or per timepoint, ``considerTimePointsAsUnit``, :252-290), each
+pairwise match's inliers added to both tiles (:292-305), the registration type's
+tiles fixed (:220-250), then ``TileConfiguration.preAlign()`` and
+``optimize(10, 10000, 200)`` (:66-78).  ``Tile``/``TileConfiguration`` and the
+model fits live in mpicbg (a third-party dependency absent from /root/reference);
+their published algorithms are restated here:
+
+  * Tile.fitModel: the tile's model is fitted to its matches, local point ->
+    the partner point as the partner tile's current model maps it; Tile.apply
+    then updates this tile's transformed points.  The tiles are visited in order
+    and each applies at once (Gauss-Seidel).
+  * Tile.updateCost: distance = the unweighted mean over the tile's matches of
+    |model(p) - partner_model(q)|; TileConfiguration.error = mean over tiles.
+  * optimize(maxAllowedError, maxIterations, maxPlateauWidth): iterate; after
+    maxPlateauWidth iterations stop once error <= maxAllowedError and the
+    error's slope over d = w, w/2, ..., 1 iterations is <= 1e-4 everywhere.
+  * preAlign: starting from the fixed tiles (or the first tile), each tile
+    connected to aligned tiles is fitted to its matches with them, breadth first;
+    the tiles never reached are returned.
+  * TranslationModel3D (weighted mean offset), RigidModel3D (Horn's closed-form
+    unit quaternion, weighted), AffineModel3D (weighted least squares about the
+    weighted centroids); 1 / 3 / 4 matches minimum.
+
+Parity unpinned: mpicbg is not in the reference tree and the reference has no
+fixtures for this stage; the tests check exact recovery of known models.
+
+This is CPU work in the reference too (SURVEY 8f keeps registration on the host):
+a few thousand correspondences per timepoint, milliseconds in numpy.  Points are
+(x, y, z) in the frame the views' current models map them to; the returned tile
+models are the corrections to pre-concatenate onto those models (the fixed tiles
+keep the identity).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+MIN_MATCHES = {"translation": 1, "rigid": 3, "affine": 4}
+
+
+class NotEnoughDataPoints(ValueError):
+    """mpicbg NotEnoughDataPointsException."""
+
+
+class IllDefinedDataPoints(ValueError):
+    """mpicbg IllDefinedDataPointsException (a singular affine system)."""
+
+
+def _identity():
+    return np.hstack([np.eye(3), np.zeros((3, 1))])
+
+
+def apply(m, pts):
+    return pts @ m[:, :3].T + m[:, 3]
+
+
+def fit(kind: str, p, q, w):
+    """The 3x4 model of ``kind`` that maps p onto q, least squares weighted by w."""
+    p, q, w = np.asarray(p, np.float64), np.asarray(q, np.float64), np.asarray(w, np.float64)
+    if len(p) < MIN_MATCHES[kind]:
+        raise NotEnoughDataPoints(f"{len(p)} matches, {kind} needs {MIN_MATCHES[kind]}")
+    ws = w.sum()
+    pc, qc = (w @ p) / ws, (w @ q) / ws
+    m = _identity()
+    if kind == "translation":
+        m[:, 3] = qc - pc
+        return m
+    dp, dq = p - pc, q - qc
+    if kind == "rigid":
+        s = (dp * w[:, None]).T @ dq                   # S[a, b] = sum w p_a q_b
+        sxx, sxy, sxz, syx, syy, syz, szx, szy, szz = s.ravel()
+        n = np.array([[sxx + syy + szz, syz - szy, szx - sxz, sxy - syx],
+                      [syz - szy, sxx - syy - szz, sxy + syx, szx + sxz],
+                      [szx - sxz, sxy + syx, -sxx + syy - szz, syz + szy],
+                      [sxy - syx, szx + sxz, syz + szy, -sxx - syy + szz]])
+        _, vec = np.linalg.eigh(n)
+        q0, qx, qy, qz = vec[:, -1]                    # the largest eigenvalue's unit quaternion
+        r = np.array([[q0 * q0 + qx * qx - qy * qy - qz * qz, 2 * (qx * qy - q0 * qz), 2 * (qx * qz + q0 * qy)],
+                      [2 * (qy * qx + q0 * qz), q0 * q0 - qx * qx + qy * qy - qz * qz, 2 * (qy * qz - q0 * qx)],
+                      [2 * (qz * qx - q0 * qy), 2 * (qz * qy + q0 * qx), q0 * q0 - qx * qx - qy * qy + qz * qz]])
+    else:
+        a = (dp * w[:, None]).T @ dp
+        b = (dp * w[:, None]).T @ dq
+        if abs(np.linalg.det(a)) < 1e-12 * max(1.0, np.abs(a).max()) ** 3:
+            raise IllDefinedDataPoints("singular point configuration for an affine fit")
+        r = np.linalg.solve(a, b).T
+    m[:, :3] = r
+    m[:, 3] = qc - r @ pc
+    return m
+
+
+@dataclass
+class PairwiseMatch:
+    """The inliers of one view pair (PairwiseMatch.getInliers): pa[i] in view a
+    corresponds to pb[i] in view b."""
+    a: int
+    b: int
+    pa: np.ndarray
+    pb: np.ndarray
+    weights: np.ndarray | None = None
+
+
+@dataclass
+class GlobalOptResult:
+    models: list          # per view: 3x4 correction (the tile's model)
+    error: float          # TileConfiguration.getError (mean tile distance)
+    min_error: float
+    max_error: float
+    iterations: int
+    unaligned: list       # views whose tile preAlign could not reach
+    tiles: list           # per view: tile index (views of one timepoint share one)
+
+
+class _Tiles:
+    def __init__(self, ntiles, kind):
+        self.kind = kind
+        self.models = [_identity() for _ in range(ntiles)]
+        # per tile: [(partner, p_local, q_partner_local, w)]
+        self.matches = [[] for _ in range(ntiles)]
+
+    def add(self, ta, tb, pa, pb, w):
+        self.matches[ta].append((tb, pa, pb, w))
+        self.matches[tb].append((ta, pb, pa, w))
+
+    def targets(self, t, only=None):
+        ps, qs, ws = [], [], []
+        for partner, p, q, w in self.matches[t]:
+            if only is not None and partner not in only:
+                continue
+            ps.append(p)
+            qs.append(apply(self.models[partner], q))
+            ws.append(w)
+        if not ps:
+            return None
+        return np.concatenate(ps), np.concatenate(qs), np.concatenate(ws)
+
+    def fit(self, t, only=None):
+        p, q, w = self.targets(t, only)
+        self.models[t] = fit(self.kind, p, q, w)
+
+    def distance(self, t):
+        p, q, _ = self.targets(t)
+        return float(np.linalg.norm(apply(self.models[t], p) - q, axis=1).mean())
+
+
+def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of=None,
+            max_allowed_error: float = 10.0, max_iterations: int = 10000,
+            max_plateau_width: int = 200) -> GlobalOptResult | None:
+    """GlobalOpt.compute over ``n_views`` views and their ``pairs`` (PairwiseMatch).
+
+    ``fixed``: the views whose tile is fixed (GlobalOptimizationType.isFixedTile);
+    ``timepoint_of``: per view its timepoint id to make one tile per timepoint
+    (considerTimePointsAsUnit), None for one tile per view.  Returns None when no
+    tile is connected (the reference prints "no connected tiles" and returns null)."""
+    if model not in MIN_MATCHES:
+        raise ValueError(f"model must be one of {sorted(MIN_MATCHES)}")
+    if timepoint_of is None:
+        tile_of = list(range(n_views))
+    else:
+        ids = {}
+        tile_of = [ids.setdefault(t, len(ids)) for t in timepoint_of]
+    ntiles = max(tile_of) + 1 if n_views else 0
+    tiles = _Tiles(ntiles, model)
+    connected = set()
+    for pm in pairs:
+        pa = np.asarray(pm.pa, np.float64).reshape(-1, 3)
+        pb = np.asarray(pm.pb, np.float64).reshape(-1, 3)
+        if len(pa) != len(pb):
+            raise ValueError("a pairwise match needs as many points in a as in b")
+        if len(pa) == 0:
+            continue
+        w = np.ones(len(pa)) if pm.weights is None else np.asarray(pm.weights, np.float64)
+        ta, tb = tile_of[pm.a], tile_of[pm.b]
+        tiles.add(ta, tb, pa, pb, w)
+        connected |= {ta, tb}
+    order = sorted(connected)                        # TileConfiguration.addTile: connected tiles
+    if not order:
+        return None
+    fixed_tiles = {tile_of[v] for v in fixed} & connected
+
+    # preAlign: breadth first from the fixed tiles (or the first tile)
+    aligned = set(fixed_tiles) if fixed_tiles else {order[0]}
+    frontier = list(aligned)
+    while frontier:
+        nxt = []
+        for t in order:
+            if t in aligned or not any(pt in aligned for pt, *_ in tiles.matches[t]):
+                continue
+            tiles.fit(t, only=aligned)
+            aligned.add(t)
+            nxt.append(t)
+        frontier = nxt
+    unaligned_tiles = [t for t in order if t not in aligned]
+
+    # optimize(maxAllowedError, maxIterations, maxPlateauWidth)
+    history = []
+    i = 0
+    proceed = i < max_iterations
+    while proceed:
+        for t in order:
+            if t not in fixed_tiles:
+                tiles.fit(t)
+        d = [tiles.distance(t) for t in order]
+        err = float(np.mean(d))
+        history.append(err)
+        if i > max_plateau_width:
+            proceed = err > max_allowed_error
+            k = max_plateau_width
+            while not proceed and k >= 1:
+                proceed |= abs((history[-1] - history[-1 - k]) / k) > 1e-4
+                k //= 2
+        i += 1
+        proceed &= i < max_iterations
+    d = [tiles.distance(t) for t in order]
+    return GlobalOptResult(models=[tiles.models[tile_of[v]] for v in range(n_views)],
+                           error=float(np.mean(d)), min_error=float(np.min(d)), max_error=float(np.max(d)),
+                           iterations=i, unaligned=[v for v in range(n_views) if tile_of[v] in unaligned_tiles],
+                           tiles=tile_of)
+
+
+def correspondences(points, models, radius: float = 2.0):
+    """Pairwise matches from detections and approximate view models: per view
+    pair, the mutual nearest neighbours within ``radius`` world pixels (an
+    ICP-style stand-in for the descriptor matching that produces the
+    reference's inliers, which stays out of scope).  Returns PairwiseMatch
+    lists over world coordinates under ``models``."""
+    from scipy.spatial import cKDTree
+    world = [apply(np.asarray(m, np.float64).reshape(3, 4), np.asarray(p, np.float64).reshape(-1, 3))
+             for p, m in zip(points, models)]
+    trees = [cKDTree(w) if len(w) else None for w in world]
+    out = []
+    for a in range(len(world)):
+        for b in range(a + 1, len(world)):
+            if trees[a] is None or trees[b] is None:
+                continue
+            dab, jab = trees[b].query(world[a], distance_upper_bound=radius)
+            dba, jba = trees[a].query(world[b], distance_upper_bound=radius)
+            ia = np.nonzero(np.isfinite(dab))[0]
+            ia = ia[jba[jab[ia]] == ia]               # mutual nearest neighbours
+            if len(ia):
+                out.append(PairwiseMatch(a, b, world[a][ia], world[b][jab[ia]]))
+    return out
+
+
+def concatenate(correction, model):
+    """correction o model, both 3x4 (the refined view model)."""
+    c, m = np.asarray(correction, np.float64), np.asarray(model, np.float64).reshape(3, 4)
+    out = np.empty((3, 4))
+    out[:, :3] = c[:, :3] @ m[:, :3]
+    out[:, 3] = c[:, :3] @ m[:, 3] + c[:, 3]
+    return out

@@ -4,11 +4,14 @@ The Fiji workflow the reference runs per timepoint, restated over this library:
 
   1. Detect Interest Points   ProcessDOG.compute per view (spim/process/interestpointdetection/
                               ProcessDOG.java:40-178) -> bead positions in view pixels
-  2. Register                 out of scope (GlobalOpt and descriptor matching run on the CPU,
-                              SURVEY 8f): the view models are given; the correspondences the
-                              registration would record are recovered from them (a detection
-                              corresponds when another view detected a bead within ``radius``
-                              world pixels of it)
+  2. Register                 the view models are given (descriptor matching stays out of
+                              scope); the correspondences the registration would
+                              record are recovered from them (a detection corresponds when
+                              another view detected a bead within ``radius`` world pixels of
+                              it).  With ``refine`` = "translation" / "rigid" / "affine" the
+                              given models are first refined on the host: mutual nearest
+                              detections -> GlobalOpt.compute (globalopt.py, GlobalOpt.java:
+                              44-135), view 0 fixed
   3. Input preparation        ProcessForDeconvolution.fuseStacksAndGetPSFs (:159-384): views
                               resampled into the bounding box, blending weights normalised,
                               and per view the PSF extracted from its corresponding beads
@@ -43,6 +46,8 @@ class TimepointResult:
     ms: dict = field(default_factory=dict)   # stage wall times
     engine: dict = field(default_factory=dict)   # RL FFT dims and z / x pass modes
     stage_digests: dict = field(default_factory=dict)   # SHA-256 per stage output (digest=True)
+    models: list = field(default_factory=list)   # the view models used (refined when refine is set)
+    globalopt: object = None                     # globalopt.GlobalOptResult (refine is set)
 
 
 def apply_model(model, pts):
@@ -99,7 +104,7 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
                       threshold: float = 0.008, localization: int = 1, radius: float = 2.0,
                       blending_border=(-8, -8, -8), blending_range=(12, 12, 12),
                       weight_type=input_prep.WeightType.VIRTUAL_WEIGHTS, device: int = 0,
-                      log=None, digest: bool = False) -> TimepointResult:
+                      log=None, digest: bool = False, refine: str | None = None) -> TimepointResult:
     """views: per view a [z, y, x] float32 torch tensor on the GPU (the acquired
     stack); models: 3x4 view -> world affines; bb_min / bb_dims (x, y, z)."""
     import torch
@@ -120,6 +125,15 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
                                            device=device)
         points.append(pos)
     t = lap("detect", t)
+    gres = None
+    models = [np.asarray(m, np.float64).reshape(3, 4) for m in models]
+    if refine is not None:   # 2'. GlobalOpt over mutual-nearest detections (host)
+        from . import globalopt
+        gres = globalopt.compute(len(models), globalopt.correspondences(points, models, radius),
+                                 model=refine, fixed=(0,))
+        if gres is not None:
+            models = [globalopt.concatenate(c, m) for c, m in zip(gres.models, models)]
+        t = lap("register", t)
     corr = corresponding_detections(points, models, radius, device=f"cuda:{device}")   # 2. (registration given)
     t = lap("correspondences", t)
     imgs, ws, info = input_prep.prepare_inputs(views, models, bb_min, bb_dims, blending_border, blending_range,
@@ -162,7 +176,7 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
         sess.close()
     del imgs, ws
     lap("rl_result", t)
-    return TimepointResult(psi, points, corr, psfs, stats, ms, engine, sd)
+    return TimepointResult(psi, points, corr, psfs, stats, ms, engine, sd, models, gres)
 
 
 def _sha(parts) -> str:

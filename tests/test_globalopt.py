@@ -1,0 +1,152 @@
+"""GlobalOpt restatement (host side, GlobalOpt.java:44-135 over mpicbg's TileConfiguration).
+
+Parity unpinned (mpicbg is absent and the reference holds no fixtures for this
+stage): the tests recover known models exactly from noiseless correspondences,
+check the fixed tile, the per-timepoint tiles, preAlign's unreachable tiles and
+the model fits' minimum match counts.
+"""
+import numpy as np
+import pytest
+
+from spim_registration_amd import globalopt as go
+
+
+def rot(ax, ay, az):
+    cx, sx, cy, sy, cz, sz = np.cos(ax), np.sin(ax), np.cos(ay), np.sin(ay), np.cos(az), np.sin(az)
+    rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return rz @ ry @ rx
+
+
+def model(kind, rng):
+    m = np.zeros((3, 4))
+    m[:, 3] = rng.uniform(-20, 20, 3)
+    if kind == "translation":
+        m[:, :3] = np.eye(3)
+    elif kind == "rigid":
+        m[:, :3] = rot(*rng.uniform(-0.3, 0.3, 3))
+    else:
+        m[:, :3] = rot(*rng.uniform(-0.3, 0.3, 3)) @ np.diag(rng.uniform(0.9, 1.1, 3)) + rng.uniform(-0.05, 0.05, (3, 3))
+    return m
+
+
+def inverse(m):
+    a = np.linalg.inv(m[:, :3])
+    return np.hstack([a, (-a @ m[:, 3])[:, None]])
+
+
+def scene(kind, views=4, beads=60, seed=0, noise=0.0):
+    """Views see the beads through the inverse of their true correction; view 0
+    is the reference frame.  Every pair shares the beads each view sees."""
+    rng = np.random.default_rng(seed)
+    b = rng.uniform(0, 400, (beads, 3))
+    truth = [go._identity()] + [model(kind, rng) for _ in range(views - 1)]
+    seen = [go.apply(inverse(t), b) + rng.normal(0, noise, b.shape) for t in truth]
+    pairs = [go.PairwiseMatch(a, c, seen[a], seen[c]) for a in range(views) for c in range(a + 1, views)]
+    return truth, pairs
+
+
+@pytest.mark.parametrize("kind", ["translation", "rigid", "affine"])
+def test_fit_recovers_model(kind):
+    rng = np.random.default_rng(3)
+    m = model(kind, rng)
+    p = rng.uniform(0, 100, (40, 3))
+    got = go.fit(kind, p, go.apply(m, p), np.ones(len(p)))
+    assert np.abs(got - m).max() < 1e-9
+    if kind == "rigid":
+        assert abs(np.linalg.det(got[:, :3]) - 1) < 1e-12
+
+
+@pytest.mark.parametrize("kind", ["translation", "rigid", "affine"])
+def test_compute_recovers_models_view0_fixed(kind):
+    truth, pairs = scene(kind)
+    res = go.compute(4, pairs, model=kind, fixed=(0,))
+    assert res.unaligned == []
+    assert np.abs(res.models[0] - go._identity()).max() == 0      # the fixed tile keeps the identity
+    for m, t in zip(res.models, truth):
+        assert np.abs(m - t).max() < 1e-6
+    assert res.error < 1e-6 and res.max_error < 1e-6
+
+
+def test_compute_noisy_converges_and_stops():
+    truth, pairs = scene("affine", noise=0.3, seed=5)
+    res = go.compute(4, pairs, model="affine")
+    assert 200 < res.iterations < 10000                           # the plateau test ends it
+    # the residual of two noisy points: 3-D distance of N(0, 2 * 0.3^2) per axis, mean 2 * 0.424 * sqrt(2 / pi) = 0.68
+    assert 0.55 < res.error < 0.75
+    for m, t in zip(res.models[1:], truth[1:]):
+        assert np.abs(m[:, 3] - t[:, 3]).max() < 2.0
+
+
+def test_rigid_weighted_fit_matches_unweighted_duplicate():
+    rng = np.random.default_rng(8)
+    p = rng.uniform(0, 50, (10, 3))
+    q = go.apply(model("rigid", rng), p) + rng.normal(0, 0.5, p.shape)
+    w = np.ones(10)
+    w[:3] = 2.0
+    a = go.fit("rigid", p, q, w)
+    b = go.fit("rigid", np.vstack([p, p[:3]]), np.vstack([q, q[:3]]), np.ones(13))
+    assert np.abs(a - b).max() < 1e-9
+
+
+def test_minimum_matches_and_ill_defined():
+    p = np.arange(9, dtype=float).reshape(3, 3)
+    with pytest.raises(go.NotEnoughDataPoints):
+        go.fit("affine", p, p, np.ones(3))
+    with pytest.raises(go.NotEnoughDataPoints):
+        go.fit("rigid", p[:2], p[:2], np.ones(2))
+    coplanar = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0.0]])
+    with pytest.raises(go.IllDefinedDataPoints):
+        go.fit("affine", coplanar, coplanar, np.ones(4))
+
+
+def test_timepoints_as_unit_share_a_tile():
+    """Views 0, 1 (timepoint 0) and 2, 3 (timepoint 1): one correction per timepoint."""
+    rng = np.random.default_rng(4)
+    b = rng.uniform(0, 400, (50, 3))
+    t1 = model("rigid", rng)
+    seen = [b[:30], b[20:], go.apply(inverse(t1), b[:35]), go.apply(inverse(t1), b[15:])]
+    pairs = []
+    for a, c in [(0, 2), (0, 3), (1, 2), (1, 3)]:
+        ia = np.arange(50)[[0, 20, 0, 15][a]:[30, 50, 35, 50][a]]
+        ic = np.arange(50)[[0, 20, 0, 15][c]:[30, 50, 35, 50][c]]
+        common = np.intersect1d(ia, ic)
+        pairs.append(go.PairwiseMatch(a, c, seen[a][common - ia[0]], seen[c][common - ic[0]]))
+    res = go.compute(4, pairs, model="rigid", fixed=(0,), timepoint_of=[0, 0, 1, 1])
+    assert res.tiles == [0, 0, 1, 1]
+    assert np.abs(res.models[1] - go._identity()).max() == 0      # fixed with view 0's tile
+    assert np.abs(res.models[2] - t1).max() < 1e-6
+    assert res.models[2] is res.models[3]
+
+
+def test_disconnected_and_empty():
+    truth, pairs = scene("rigid", views=3)
+    pairs = [p for p in pairs if p.a == 0 and p.b == 1]
+    res = go.compute(3, pairs, model="rigid")
+    assert res.unaligned == []                  # view 2 has no tile in the configuration
+    assert np.abs(res.models[2] - go._identity()).max() == 0
+    assert go.compute(3, [], model="rigid") is None
+    # two separate components: the one without a fixed tile is never reached by preAlign
+    _, p4 = scene("translation", views=4)
+    comp = [p for p in p4 if (p.a, p.b) in ((0, 1), (2, 3))]
+    res = go.compute(4, comp, model="translation", fixed=(0,), max_iterations=5)
+    assert res.unaligned == [2, 3]
+
+
+def test_correspondences_then_refine():
+    """Approximate models (truth + a 0.8-pixel offset) -> mutual-nearest matches ->
+    GlobalOpt -> refined models within 1e-6 of the truth."""
+    rng = np.random.default_rng(11)
+    b = rng.uniform(0, 300, (80, 3))
+    truth = [go._identity()] + [model("rigid", rng) for _ in range(2)]
+    points = [go.apply(inverse(t), b) for t in truth]
+    approx = [t.copy() for t in truth]
+    approx[1][:, 3] += 0.8
+    approx[2][:, 3] -= 0.5
+    pairs = go.correspondences(points, approx, radius=3.0)
+    assert [(p.a, p.b, len(p.pa)) for p in pairs] == [(0, 1, 80), (0, 2, 80), (1, 2, 80)]
+    res = go.compute(3, pairs, model="rigid", fixed=(0,))
+    refined = [go.concatenate(c, m) for c, m in zip(res.models, approx)]
+    for m, t in zip(refined, truth):
+        assert np.abs(m - t).max() < 1e-6
