@@ -28,8 +28,11 @@ their published algorithms are restated here:
 Parity unpinned: mpicbg is not in the reference tree and the reference has no
 fixtures for this stage; the tests check exact recovery of known models.
 
-This is CPU work in the reference too (SURVEY 8f keeps registration on the host):
-a few thousand correspondences per timepoint, milliseconds in numpy.  Points are
+This is CPU work in the reference too (SURVEY 8f keeps registration on the host).
+A tile's fit runs on per-partner moments (3x3 algebra per pair), so an iteration
+costs one distance evaluation per match: 8 views with 20,000 beads each (28
+pairs, 560k matches) take 7-8 s for the 202 iterations the plateau test needs
+(this container, one thread).  Points are
 (x, y, z) in the frame the views' current models map them to; the returned tile
 models are the corrections to pre-concatenate onto those models (the fixed tiles
 keep the identity).
@@ -62,33 +65,40 @@ def apply(m, pts):
 def fit(kind: str, p, q, w):
     """The 3x4 model of ``kind`` that maps p onto q, least squares weighted by w."""
     p, q, w = np.asarray(p, np.float64), np.asarray(q, np.float64), np.asarray(w, np.float64)
-    if len(p) < MIN_MATCHES[kind]:
-        raise NotEnoughDataPoints(f"{len(p)} matches, {kind} needs {MIN_MATCHES[kind]}")
-    ws = w.sum()
-    pc, qc = (w @ p) / ws, (w @ q) / ws
+    return _fit_moments(kind, len(p), *_moments(p, q, w))
+
+
+def _moments(p, q, w):
+    """(sum w, sum w p, sum w q, sum w p p^T, sum w p q^T): all a fit needs."""
+    wp = p * w[:, None]
+    return w.sum(), wp.sum(axis=0), w @ q, wp.T @ p, wp.T @ q
+
+
+def _fit_moments(kind, n, ws, sp, sq, spp, spq):
+    if n < MIN_MATCHES[kind]:
+        raise NotEnoughDataPoints(f"{n} matches, {kind} needs {MIN_MATCHES[kind]}")
+    pc, qc = sp / ws, sq / ws
     m = _identity()
     if kind == "translation":
         m[:, 3] = qc - pc
         return m
-    dp, dq = p - pc, q - qc
+    s = spq - ws * np.outer(pc, qc)                    # sum w (p - pc)(q - qc)^T
     if kind == "rigid":
-        s = (dp * w[:, None]).T @ dq                   # S[a, b] = sum w p_a q_b
         sxx, sxy, sxz, syx, syy, syz, szx, szy, szz = s.ravel()
-        n = np.array([[sxx + syy + szz, syz - szy, szx - sxz, sxy - syx],
-                      [syz - szy, sxx - syy - szz, sxy + syx, szx + sxz],
-                      [szx - sxz, sxy + syx, -sxx + syy - szz, syz + szy],
-                      [sxy - syx, szx + sxz, syz + szy, -sxx - syy + szz]])
-        _, vec = np.linalg.eigh(n)
+        nm = np.array([[sxx + syy + szz, syz - szy, szx - sxz, sxy - syx],
+                       [syz - szy, sxx - syy - szz, sxy + syx, szx + sxz],
+                       [szx - sxz, sxy + syx, -sxx + syy - szz, syz + szy],
+                       [sxy - syx, szx + sxz, syz + szy, -sxx - syy + szz]])
+        _, vec = np.linalg.eigh(nm)
         q0, qx, qy, qz = vec[:, -1]                    # the largest eigenvalue's unit quaternion
         r = np.array([[q0 * q0 + qx * qx - qy * qy - qz * qz, 2 * (qx * qy - q0 * qz), 2 * (qx * qz + q0 * qy)],
                       [2 * (qy * qx + q0 * qz), q0 * q0 - qx * qx + qy * qy - qz * qz, 2 * (qy * qz - q0 * qx)],
                       [2 * (qz * qx - q0 * qy), 2 * (qz * qy + q0 * qx), q0 * q0 - qx * qx - qy * qy + qz * qz]])
     else:
-        a = (dp * w[:, None]).T @ dp
-        b = (dp * w[:, None]).T @ dq
+        a = spp - ws * np.outer(pc, pc)                # sum w (p - pc)(p - pc)^T
         if abs(np.linalg.det(a)) < 1e-12 * max(1.0, np.abs(a).max()) ** 3:
             raise IllDefinedDataPoints("singular point configuration for an affine fit")
-        r = np.linalg.solve(a, b).T
+        r = np.linalg.solve(a, s).T
     m[:, :3] = r
     m[:, 3] = qc - r @ pc
     return m
@@ -117,35 +127,49 @@ class GlobalOptResult:
 
 
 class _Tiles:
+    """The tiles' models and matches.  A match's partner point moves only with
+    the partner's (affine) model, so a tile's fit needs per partner only the
+    moments of its local points against the partner's local points; the
+    distances are evaluated per pair (both tiles of a pair share them)."""
+
     def __init__(self, ntiles, kind):
         self.kind = kind
         self.models = [_identity() for _ in range(ntiles)]
-        # per tile: [(partner, p_local, q_partner_local, w)]
-        self.matches = [[] for _ in range(ntiles)]
+        self.pairs = []                          # (ta, tb, pa, pb)
+        self.sides = [[] for _ in range(ntiles)]  # per tile: (partner, n, moments of own vs partner points)
 
     def add(self, ta, tb, pa, pb, w):
-        self.matches[ta].append((tb, pa, pb, w))
-        self.matches[tb].append((ta, pb, pa, w))
-
-    def targets(self, t, only=None):
-        ps, qs, ws = [], [], []
-        for partner, p, q, w in self.matches[t]:
-            if only is not None and partner not in only:
-                continue
-            ps.append(p)
-            qs.append(apply(self.models[partner], q))
-            ws.append(w)
-        if not ps:
-            return None
-        return np.concatenate(ps), np.concatenate(qs), np.concatenate(ws)
+        self.pairs.append((ta, tb, pa, pb))
+        self.sides[ta].append((tb, len(pa), _moments(pa, pb, w)))
+        self.sides[tb].append((ta, len(pa), _moments(pb, pa, w)))
 
     def fit(self, t, only=None):
-        p, q, w = self.targets(t, only)
-        self.models[t] = fit(self.kind, p, q, w)
+        n, ws, sp, sq, spp, spq = 0, 0.0, np.zeros(3), np.zeros(3), np.zeros((3, 3)), np.zeros((3, 3))
+        for partner, k, (w0, p1, q1, pp, pq) in self.sides[t]:
+            if only is not None and partner not in only:
+                continue
+            a, tr = self.models[partner][:, :3], self.models[partner][:, 3]
+            n += k
+            ws += w0
+            sp = sp + p1
+            sq = sq + a @ q1 + w0 * tr
+            spp = spp + pp
+            spq = spq + pq @ a.T + np.outer(p1, tr)
+        self.models[t] = _fit_moments(self.kind, n, ws, sp, sq, spp, spq)
 
-    def distance(self, t):
-        p, q, _ = self.targets(t)
-        return float(np.linalg.norm(apply(self.models[t], p) - q, axis=1).mean())
+    def partners(self, t):
+        return [partner for partner, *_ in self.sides[t]]
+
+    def distances(self, ntiles):
+        """Per tile Tile.getDistance: the mean over its matches of |model(p) - partner_model(q)|."""
+        tot, cnt = np.zeros(ntiles), np.zeros(ntiles)
+        for ta, tb, pa, pb in self.pairs:
+            d = np.linalg.norm(apply(self.models[ta], pa) - apply(self.models[tb], pb), axis=1).sum()
+            tot[ta] += d
+            tot[tb] += d
+            cnt[ta] += len(pa)
+            cnt[tb] += len(pa)
+        return tot, cnt
 
 
 def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of=None,
@@ -189,7 +213,7 @@ def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of
     while frontier:
         nxt = []
         for t in order:
-            if t in aligned or not any(pt in aligned for pt, *_ in tiles.matches[t]):
+            if t in aligned or not any(pt in aligned for pt in tiles.partners(t)):
                 continue
             tiles.fit(t, only=aligned)
             aligned.add(t)
@@ -205,8 +229,8 @@ def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of
         for t in order:
             if t not in fixed_tiles:
                 tiles.fit(t)
-        d = [tiles.distance(t) for t in order]
-        err = float(np.mean(d))
+        tot, cnt = tiles.distances(ntiles)
+        err = float(np.mean(tot[order] / cnt[order]))
         history.append(err)
         if i > max_plateau_width:
             proceed = err > max_allowed_error
@@ -216,7 +240,8 @@ def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of
                 k //= 2
         i += 1
         proceed &= i < max_iterations
-    d = [tiles.distance(t) for t in order]
+    tot, cnt = tiles.distances(ntiles)
+    d = tot[order] / cnt[order]
     return GlobalOptResult(models=[tiles.models[tile_of[v]] for v in range(n_views)],
                            error=float(np.mean(d)), min_error=float(np.min(d)), max_error=float(np.max(d)),
                            iterations=i, unaligned=[v for v in range(n_views) if tile_of[v] in unaligned_tiles],
