@@ -182,7 +182,12 @@ def load():
     together with this library must load torch's copy first so both share one
     HIP runtime: the reverse order hands torch the /opt/rocm runtime, and the
     process aborts at exit ("double free or corruption") after a torch GPU
-    call.  load() therefore imports torch (when installed) before the library."""
+    call.  load() therefore imports torch (when installed) before the library.
+
+    SPIMDECON_HIP_RUNTIME=system skips that import: the library then binds the
+    ROCm stack it was linked against (/opt/rocm, the rpath), which is what a
+    JNA consumer without torch loads (tests/jna_child.py).
+    Such a process must not use torch on the GPU."""
     global _lib
     if _lib is not None:
         return _lib
@@ -190,10 +195,11 @@ def load():
         raise RuntimeError(
             f"{LIB_PATH} not found: build it with `python -m spim_registration_amd.build` "
             "(there is no CPU fallback)")
-    try:
-        import torch  # noqa: F401  (binds the HIP runtime soname to torch's copy)
-    except ImportError:
-        pass
+    if os.environ.get("SPIMDECON_HIP_RUNTIME", "") != "system":
+        try:
+            import torch  # noqa: F401  (binds the HIP runtime soname to torch's copy)
+        except ImportError:
+            pass
     lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)

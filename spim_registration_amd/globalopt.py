@@ -18,9 +18,12 @@ their published algorithms are restated here:
   * optimize(maxAllowedError, maxIterations, maxPlateauWidth): iterate; after
     maxPlateauWidth iterations stop once error <= maxAllowedError and the
     error's slope over d = w, w/2, ..., 1 iterations is <= 1e-4 everywhere.
-  * preAlign: starting from the fixed tiles (or the first tile), each tile
-    connected to aligned tiles is fitted to its matches with them, breadth first;
-    the tiles never reached are returned.
+  * preAlign: starting from the fixed tiles (or the first tile), a list iterator
+    walks the aligned tiles; each unaligned tile connected to the current one is
+    fitted to its matches with that tile only and visited next (ListIterator.add +
+    previous); the tiles never reached are returned.
+  * a NotEnoughDataPoints / IllDefinedDataPoints from preAlign or optimize is
+    caught and printed, and the models are returned as they stand (GlobalOpt.java:92-100).
   * TranslationModel3D (weighted mean offset), RigidModel3D (Horn's closed-form
     unit quaternion, weighted), AffineModel3D (weighted least squares about the
     weighted centroids); 1 / 3 / 4 matches minimum.
@@ -124,6 +127,7 @@ class GlobalOptResult:
     iterations: int
     unaligned: list       # views whose tile preAlign could not reach
     tiles: list           # per view: tile index (views of one timepoint share one)
+    failure: str | None = None   # the caught NotEnoughDataPoints / IllDefinedDataPoints message
 
 
 class _Tiles:
@@ -207,21 +211,49 @@ def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of
         return None
     fixed_tiles = {tile_of[v] for v in fixed} & connected
 
-    # preAlign: breadth first from the fixed tiles (or the first tile)
-    aligned = set(fixed_tiles) if fixed_tiles else {order[0]}
-    frontier = list(aligned)
-    while frontier:
-        nxt = []
-        for t in order:
-            if t in aligned or not any(pt in aligned for pt in tiles.partners(t)):
-                continue
-            tiles.fit(t, only=aligned)
-            aligned.add(t)
-            nxt.append(t)
-        frontier = nxt
+    # preAlign then optimize(10, 10000, 200); a NotEnoughDataPoints / IllDefinedDataPoints
+    # from either is caught, printed and the tiles' models returned as they stand
+    # (GlobalOpt.java:64-100)
+    aligned, failure, i = [], None, 0
+    try:
+        _pre_align(tiles, order, fixed_tiles, aligned)
+        i = _optimize(tiles, order, fixed_tiles, ntiles, max_allowed_error, max_iterations, max_plateau_width)
+    except (NotEnoughDataPoints, IllDefinedDataPoints) as e:
+        failure = f"Global optimization failed: {type(e).__name__}: {e}"
+        print(failure)
     unaligned_tiles = [t for t in order if t not in aligned]
+    tot, cnt = tiles.distances(ntiles)
+    d = tot[order] / cnt[order]
+    return GlobalOptResult(models=[tiles.models[tile_of[v]] for v in range(n_views)],
+                           error=float(np.mean(d)), min_error=float(np.min(d)), max_error=float(np.max(d)),
+                           iterations=i, unaligned=[v for v in range(n_views) if tile_of[v] in unaligned_tiles],
+                           tiles=tile_of, failure=failure)
 
-    # optimize(maxAllowedError, maxIterations, maxPlateauWidth)
+
+def _pre_align(tiles, order, fixed_tiles, aligned):
+    """TileConfiguration.preAlign: walk a list of aligned tiles (the fixed ones, or the
+    first tile) with a list iterator; every unaligned tile connected to the current one is
+    fitted to its matches with that tile only, inserted at the iterator's cursor and
+    stepped back over (ListIterator.add + previous), so it is visited next.  Fills
+    ``aligned`` (so a fit that raises leaves the tiles aligned so far); the rest are the
+    ones preAlign reports as unaligned."""
+    aligned[:] = [t for t in order if t in fixed_tiles] or [order[0]]
+    unaligned = [t for t in order if t not in aligned]
+    cur = 0
+    while cur < len(aligned):
+        a = aligned[cur]
+        cur += 1                                     # ita.next()
+        partners = set(tiles.partners(a))
+        for u in list(unaligned):
+            if u in partners:
+                tiles.fit(u, only={a})
+                aligned.insert(cur, u)               # ita.add(u); ita.previous()
+                unaligned.remove(u)
+
+
+def _optimize(tiles, order, fixed_tiles, ntiles, max_allowed_error, max_iterations, max_plateau_width):
+    """TileConfiguration.optimize(maxAllowedError, maxIterations, maxPlateauWidth): the
+    number of iterations run."""
     history = []
     i = 0
     proceed = i < max_iterations
@@ -240,12 +272,7 @@ def compute(n_views: int, pairs, model: str = "affine", fixed=(0,), timepoint_of
                 k //= 2
         i += 1
         proceed &= i < max_iterations
-    tot, cnt = tiles.distances(ntiles)
-    d = tot[order] / cnt[order]
-    return GlobalOptResult(models=[tiles.models[tile_of[v]] for v in range(n_views)],
-                           error=float(np.mean(d)), min_error=float(np.min(d)), max_error=float(np.max(d)),
-                           iterations=i, unaligned=[v for v in range(n_views) if tile_of[v] in unaligned_tiles],
-                           tiles=tile_of)
+    return i
 
 
 def correspondences(points, models, radius: float = 2.0):

@@ -131,7 +131,9 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
         from . import globalopt
         gres = globalopt.compute(len(models), globalopt.correspondences(points, models, radius),
                                  model=refine, fixed=(0,))
-        if gres is not None:
+        if gres is not None:   # (a caught fit failure keeps the tiles' models as they stand, as the reference)
+            if gres.failure and log:
+                log(gres.failure)
             models = [globalopt.concatenate(c, m) for c, m in zip(gres.models, models)]
         t = lap("register", t)
     corr = corresponding_detections(points, models, radius, device=f"cuda:{device}")   # 2. (registration given)

@@ -150,3 +150,39 @@ def test_correspondences_then_refine():
     refined = [go.concatenate(c, m) for c, m in zip(res.models, approx)]
     for m, t in zip(refined, truth):
         assert np.abs(m - t).max() < 1e-6
+
+
+def test_too_few_matches_caught_models_returned():
+    """GlobalOpt.java:92-100: NotEnoughDataPoints from preAlign is caught and printed,
+    the tiles' models are returned as they stand (view 2: 2 matches, rigid needs 3)."""
+    truth, pairs = scene("rigid", views=3)
+    pairs = [p for p in pairs if (p.a, p.b) == (0, 1)] + [
+        go.PairwiseMatch(0, 2, pairs[1].pa[:2], pairs[1].pb[:2])]
+    res = go.compute(3, pairs, model="rigid", fixed=(0,))
+    assert res is not None and res.failure is not None and "NotEnoughDataPoints" in res.failure
+    assert np.abs(res.models[0] - go._identity()).max() == 0
+    assert np.abs(res.models[2] - go._identity()).max() == 0       # never fitted
+    assert res.iterations == 0                                     # optimize did not run
+    # coplanar matches under affine: IllDefinedDataPoints, caught the same way
+    cop = np.array([[0, 0, 0], [5, 0, 0], [0, 5, 0], [5, 5, 0], [2, 3, 0.0]])
+    res = go.compute(2, [go.PairwiseMatch(0, 1, cop, cop + 1.0)], model="affine")
+    assert res.failure is not None and "IllDefinedDataPoints" in res.failure
+
+
+def test_prealign_fits_to_the_reaching_tile_only():
+    """mpicbg TileConfiguration.preAlign: a newly reached tile is fitted to its matches
+    with the aligned tile that reached it, not to every aligned partner.  View 2's matches
+    with view 0 say t2, its matches with view 1 say something else: after preAlign alone
+    (no optimize iterations) view 2 holds exactly t2; a chain 0-1, 1-3 reaches 3 through 1."""
+    rng = np.random.default_rng(21)
+    b = rng.uniform(0, 300, (40, 3))
+    t1, t2, t3 = (model("rigid", rng) for _ in range(3))
+    seen0, seen1, seen2 = b, go.apply(inverse(t1), b), go.apply(inverse(t2), b)
+    other = go.apply(inverse(model("rigid", rng)), b)          # inconsistent with t2
+    pairs = [go.PairwiseMatch(0, 1, seen0, seen1), go.PairwiseMatch(0, 2, seen0, seen2),
+             go.PairwiseMatch(1, 2, seen1, other), go.PairwiseMatch(1, 3, seen1, go.apply(inverse(t3), b))]
+    res = go.compute(4, pairs, model="rigid", fixed=(0,), max_iterations=0)
+    assert res.failure is None and res.iterations == 0 and res.unaligned == []
+    assert np.abs(res.models[1] - t1).max() < 1e-6
+    assert np.abs(res.models[2] - t2).max() < 1e-6
+    assert np.abs(res.models[3] - t3).max() < 1e-6
