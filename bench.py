@@ -34,6 +34,7 @@ iterations, BASELINE.md protocol).
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -304,7 +305,8 @@ def main(argv=None):
     mode, N = plan_gpus(args, os.environ, torch.cuda.device_count())
     from spim_registration_amd import synthetic
     from spim_registration_amd.decon import PSFTYPE, Session
-    from spim_registration_amd.distributed import broadcast_comm_id, env_rank, slab_range
+    from spim_registration_amd.distributed import (broadcast_comm_id, env_rank, rank_plan, slab_range,
+                                                   verify_rank_plans)
 
     if mode == "ranks":
         rank, world, local = env_rank()
@@ -314,7 +316,8 @@ def main(argv=None):
         devices = list(range(N))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+        # control plane only; a rank that never arrives fails the others within 10 minutes
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
 
     def barrier():
         if world > 1:
@@ -376,6 +379,8 @@ def main(argv=None):
         for i, w, k in zip(imgs, ws, psfs):
             s.add_view_device(i.data_ptr(), w.data_ptr(), k)
         s.init(PSFTYPE[psftype])
+        if world > 1:   # every rank's exchange plan, before the first exchange (no mismatched RCCL waits)
+            verify_rank_plans(dist, rank_plan(s, rank, world))
         s.init_psi()
         return s
 

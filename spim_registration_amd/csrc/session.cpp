@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <exception>
 #include <thread>
 
@@ -151,6 +152,7 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
     }
     stream_ = groups_[0].stream;
     if (p_.nranks > 1) {
+        if (const char* e = std::getenv("SPIMDECON_RCCL_TIMEOUT")) rccl_timeout_s_ = std::max(1.0, std::atof(e));
         DeviceGuard guard(p_.device);
         ncclUniqueId id;
         std::memcpy(&id, p_.comm_id, sizeof(id));
@@ -174,6 +176,29 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
 }
 
 Session::~Session() {
+    if (rccl_dead_) {
+        // an aborted communicator: its kernels should drain; if a stream still holds work
+        // after 30 s, leak the buffers rather than block in hipFree (the process is failing)
+        bool busy = false;
+        for (auto& gr : groups_) {
+            DeviceGuard guard(gr.dev);
+            for (hipStream_t st : {gr.stream, gr.xstream}) {
+                const auto t0 = std::chrono::steady_clock::now();
+                while (st && hipStreamQuery(st) == hipErrorNotReady) {
+                    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+                        busy = true;
+                        break;
+                    }
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                }
+            }
+        }
+        if (busy) {
+            new std::vector<SlabState>(std::move(slabs_));   // intentionally leaked
+            new std::vector<DevGroup>(std::move(groups_));
+            return;
+        }
+    }
     for (auto& gr : groups_) {
         DeviceGuard guard(gr.dev);
         if (gr.stream) (void)hipStreamSynchronize(gr.stream);
@@ -186,6 +211,7 @@ Session::~Session() {
             (void)hipEventDestroy(r.b);
         }
         for (auto e : event_pool_) (void)hipEventDestroy(e);
+        for (auto e : progress_) (void)hipEventDestroy(e);
         if (comm_) ncclCommDestroy(comm_);
     }
     for (auto& sl : slabs_) {  // buffers and plans released on their own device
@@ -223,8 +249,8 @@ void Session::slab_extent(int slab, int64_t* out3) const {
 void Session::sync_all() {
     for (auto& gr : groups_) {
         DeviceGuard guard(gr.dev);
-        SD_HIP(hipStreamSynchronize(gr.stream));
-        SD_HIP(hipStreamSynchronize(gr.xstream));
+        wait_stream(gr.stream);
+        wait_stream(gr.xstream);
     }
 }
 
@@ -309,7 +335,7 @@ void Session::add_view(const float* img, const float* weight, const float* k1, c
                 bufs[s].push_back(std::move(buf));
             }
         }
-        SD_HIP(hipStreamSynchronize(gr.stream));
+        wait_stream(gr.stream);
     }
     for (size_t s = 0; s < slabs_.size(); ++s) {
         slabs_[s].img.push_back(std::move(bufs[s][0]));
@@ -418,7 +444,7 @@ void Session::build_spectra() {
                     DBuf<float> spec(rf);
                     launch_place_kernel(g, kd.p, hk.dims[0], hk.dims[1], hk.dims[2], scale, spec.p, stream_);
                     sl.fft->forward(spec.p);
-                    SD_HIP(hipStreamSynchronize(stream_));
+                    wait_stream(stream_);
                     (which == 0 ? sl.k1spec : sl.k2spec).push_back(std::move(spec));
                 }
             }
@@ -459,9 +485,10 @@ void Session::build_spectra() {
                 }
             }
         }
-        SD_HIP(hipStreamSynchronize(stream_));
+        wait_stream(stream_);
     }
     spectra_ready_ = true;
+    verify_ranks();
 }
 
 double Session::init_psi(const float* psi_or_null) {
@@ -482,7 +509,7 @@ double Session::init_psi(const float* psi_or_null) {
             sl.img_ptrs.alloc(nviews_);
             SD_HIP(hipMemcpyAsync(sl.img_ptrs.p, ptrs.data(), nviews_ * sizeof(void*),
                                   hipMemcpyHostToDevice, st));
-            SD_HIP(hipStreamSynchronize(st));
+            wait_stream(st);
         }
     }
     if (psi_or_null) {
@@ -492,7 +519,7 @@ double Session::init_psi(const float* psi_or_null) {
             DBuf<float> tmp;
             load_slab(psi_or_null, hipMemcpyHostToDevice, sl, sl.psi, tmp, st);
             launch_clamp_min(sl.psi, sl.n, st);
-            SD_HIP(hipStreamSynchronize(st));
+            wait_stream(st);
         }
     } else {
         // FirstIteration + fuseFirstIteration (MVDeconvolution.java:192-235)
@@ -505,7 +532,7 @@ double Session::init_psi(const float* psi_or_null) {
             const int64_t nb = launch_first_iteration(sl.n, nviews_, store_, sl.img_ptrs.p, dpart.p, st);
             part.resize(2 * nb);
             SD_HIP(hipMemcpyAsync(part.data(), dpart.p, part.size() * 8, hipMemcpyDeviceToHost, st));
-            SD_HIP(hipStreamSynchronize(st));
+            wait_stream(st);
             for (int64_t i = 0; i < nb; ++i) {
                 acc[0] += part[2 * i];
                 acc[1] += part[2 * i + 1];
@@ -723,7 +750,7 @@ void Session::allreduce_sum(double* host, int n) {
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
     SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclSum, comm_, stream_));
     SD_HIP(hipMemcpyAsync(host, d.p, n * 8, hipMemcpyDeviceToHost, stream_));
-    SD_HIP(hipStreamSynchronize(stream_));
+    wait_stream(stream_);
 }
 
 void Session::allreduce_max(double* host, int n) {
@@ -733,7 +760,101 @@ void Session::allreduce_max(double* host, int n) {
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
     SD_NCCL(ncclAllReduce(d.p, d.p, n, ncclDouble, ncclMax, comm_, stream_));
     SD_HIP(hipMemcpyAsync(host, d.p, n * 8, hipMemcpyDeviceToHost, stream_));
-    SD_HIP(hipStreamSynchronize(stream_));
+    wait_stream(stream_);
+}
+
+void Session::record_progress(hipStream_t st) {
+    if (!comm_) return;
+    if (nprogress_ == progress_.size()) {
+        hipEvent_t e;
+        SD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        progress_.push_back(e);
+    }
+    SD_HIP(hipEventRecord(progress_[nprogress_++], st));
+}
+
+void Session::wait_stream(hipStream_t st) {
+    if (!comm_) {
+        SD_HIP(hipStreamSynchronize(st));
+        return;
+    }
+    using clk = std::chrono::steady_clock;
+    auto last = clk::now();
+    size_t done = 0;   // progress events seen complete
+    int spins = 0;
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) SD_HIP(e);
+        while (done < nprogress_ && hipEventQuery(progress_[done]) == hipSuccess) {
+            ++done;
+            last = clk::now();
+        }
+        ncclResult_t ar = ncclSuccess;
+        (void)ncclCommGetAsyncError(comm_, &ar);
+        const double idle = std::chrono::duration<double>(clk::now() - last).count();
+        if ((ar != ncclSuccess && ar != ncclInProgress) || idle > rccl_timeout_s_) {
+            const std::string why = ar != ncclSuccess && ar != ncclInProgress
+                                        ? std::string("RCCL asynchronous error: ") + ncclGetErrorString(ar)
+                                        : "no progress for " + std::to_string(int(idle)) +
+                                              " s (SPIMDECON_RCCL_TIMEOUT): mismatched halo exchanges across ranks?";
+            (void)ncclCommAbort(comm_);
+            comm_ = nullptr;
+            rccl_dead_ = true;
+            poisoned_ = true;
+            fail(SPIMDECON_ERR_COMM, "rank " + std::to_string(p_.rank) + ": " + why + "; communicator aborted");
+        }
+        // spin briefly (a run's last iteration usually ends within microseconds), then sleep
+        if (++spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (st == stream_) nprogress_ = 0;
+}
+
+// the exchange geometry of this rank, all-gathered; refused on every rank when any two
+// ranks' sends and receives could not match (they would wait for each other forever)
+void Session::verify_ranks() {
+    if (p_.nranks <= 1 || !comm_) return;
+    constexpr int K = 12;
+    int64_t ext = 0;
+    for (auto& sl : slabs_) ext += sl.g.nz;
+    const int64_t mine[K] = {0x5350494d44454301LL, p_.nranks, p_.rank, p_.nz_global, p_.z_offset, ext,
+                             int64_t(axis_), int64_t(store_ == Store::F16), int64_t(backend_), int64_t(nviews_),
+                             int64_t(halo_[2]), int64_t(plane_floats())};
+    DeviceGuard guard(p_.device);
+    const int R = p_.nranks;
+    DBuf<int64_t> d(size_t(K) * R);
+    std::vector<int64_t> all(size_t(K) * R, 0);
+    SD_HIP(hipMemcpyAsync(d.p + size_t(K) * p_.rank, mine, sizeof(mine), hipMemcpyHostToDevice, stream_));
+    SD_NCCL(ncclAllGather(d.p + size_t(K) * p_.rank, d.p, K, ncclInt64, comm_, stream_));
+    SD_HIP(hipMemcpyAsync(all.data(), d.p, all.size() * 8, hipMemcpyDeviceToHost, stream_));
+    wait_stream(stream_);
+    static const char* names[K] = {"build", "nranks", "rank", "nz_global", "z_offset", "extent", "slab_axis",
+                                   "storage_fp16", "fft_backend", "views", "halo planes", "plane floats"};
+    std::string bad;
+    for (int r = 0; r < R && bad.empty(); ++r) {
+        const int64_t* q = all.data() + size_t(K) * r;
+        for (int k = 0; k < K; ++k) {
+            const bool must_equal = k != 2 && k != 4 && k != 5;
+            if ((must_equal && q[k] != mine[k]) || (k == 2 && q[k] != r)) {
+                bad = std::string(names[k]) + ": rank " + std::to_string(r) + " has " + std::to_string(q[k]) +
+                      ", rank " + std::to_string(p_.rank) + " has " + std::to_string(mine[k]);
+                break;
+            }
+        }
+        if (bad.empty() && r + 1 < R) {   // adjacent ranks own adjacent ranges
+            const int64_t* n = q + K;
+            if (q[4] + q[5] != n[4])
+                bad = "rank " + std::to_string(r) + " owns [" + std::to_string(q[4]) + ", " +
+                      std::to_string(q[4] + q[5]) + ") but rank " + std::to_string(r + 1) + " starts at " +
+                      std::to_string(n[4]);
+        }
+    }
+    if (bad.empty()) {
+        const int64_t* l = all.data() + size_t(K) * (R - 1);
+        if (all[4] != 0 || l[4] + l[5] != p_.nz_global)
+            bad = "the ranks' ranges do not cover [0, nz_global)";
+    }
+    SD_CHECK(bad.empty(), SPIMDECON_ERR_ARG, "ranks disagree on the exchange geometry (" + bad + ")");
 }
 
 void Session::run(int iters, double lambda, double* stats) {
@@ -743,6 +864,7 @@ void Session::run(int iters, double lambda, double* stats) {
     SD_CHECK(psi_ready_, SPIMDECON_ERR_STATE, "call mvd_init_psi first");
     if (iters == 0) return;
     const int V = nviews_;
+    nprogress_ = 0;
     for (auto& gr : groups_) {
         DeviceGuard guard(gr.dev);
         gr.stats.alloc(size_t(iters) * V * 2);
@@ -790,7 +912,7 @@ void Session::run(int iters, double lambda, double* stats) {
         DevGroup& gr = groups_[gi];
         DeviceGuard guard(gr.dev);
         SD_HIP(hipMemcpyAsync(part.data(), gr.stats.p, part.size() * 8, hipMemcpyDeviceToHost, gr.stream));
-        SD_HIP(hipStreamSynchronize(gr.stream));
+        wait_stream(gr.stream);
         for (size_t i = 0; i < st.size(); i += 2) {
             st[i] = gi == 0 ? part[i] : st[i] + part[i];
             st[i + 1] = gi == 0 ? part[i + 1] : std::max(st[i + 1], part[i + 1]);
@@ -894,6 +1016,7 @@ void Session::run_rocfft(int iters, double lambda) {
             }
             if (!last) exchange(true, stream_);
         }
+        record_progress(stream_);
     }
 }
 
@@ -1050,6 +1173,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             if (ov) pending = true;  // ended inside the next view's convolve_all
             else if (!last) xfull(true);
         }
+        record_progress(st);   // (RCCL watchdog: one event per iteration)
     }
 }
 
@@ -1071,7 +1195,7 @@ void Session::get_psi(float* out) {
         DeviceGuard guard(groups_[sl.grp].dev);
         DBuf<float> tmp;
         store_slab(sl, sl.psi, out, tmp, groups_[sl.grp].stream);
-        SD_HIP(hipStreamSynchronize(groups_[sl.grp].stream));
+        wait_stream(groups_[sl.grp].stream);
     }
 }
 

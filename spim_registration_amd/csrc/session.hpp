@@ -194,6 +194,21 @@ private:
     double tacc_[16] = {0};
     std::vector<hipEvent_t> event_pool_;
     hipEvent_t get_event();
+
+    // RCCL watchdog (nranks > 1).  Every host wait on a stream that RCCL work feeds is
+    // bounded: when the stream's progress events (one per RL iteration) stop completing
+    // for rccl_timeout_s_ seconds, or RCCL reports an asynchronous error, the communicator
+    // is aborted (ncclCommAbort) and the call fails with SPIMDECON_ERR_COMM -- ranks whose
+    // sends and receives do not match fail instead of waiting forever.
+    double rccl_timeout_s_ = 300.0;  // SPIMDECON_RCCL_TIMEOUT (seconds)
+    bool rccl_dead_ = false;          // aborted: the session's streams may hold dead work
+    std::vector<hipEvent_t> progress_;  // recorded on the compute stream after each iteration
+    size_t nprogress_ = 0;              // progress_ entries recorded in the current run
+    void wait_stream(hipStream_t st);
+    void record_progress(hipStream_t st);
+    // all-gathers every rank's exchange geometry (RCCL) once the spectra are built and
+    // fails on every rank when they disagree (counts, halo planes, z ranges, views)
+    void verify_ranks();
 };
 
 }  // namespace spimdecon

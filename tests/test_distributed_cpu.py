@@ -215,3 +215,81 @@ def test_halo_plan_rejects_bad_geometry():
     from spim_registration_amd import _lib
     with pytest.raises(_lib.SpimDeconError):
         halo_plan(10, 20, 6, 4)      # Mz < nz + 2 cz
+
+
+# ------------------------------------------------------- rank consistency before exchanging
+# bench.py all-gathers every rank's exchange plan (distributed.rank_plan) over the gloo
+# control group after mvd_init and refuses to start when they disagree, so ranks can never
+# post mismatched ncclSend / ncclRecv and wait forever.  The plans here are what rank_plan
+# returns for C3's 8-rank y-slab decomposition (1024 rows -> 128 + 2 * 12 per rank).
+
+from spim_registration_amd.distributed import check_rank_plans, verify_rank_plans  # noqa: E402
+
+
+def _c3_plan(rank, world=8, nglob=1024, cz=12, Mx=1050, My=540, nviews=6, zmode=3):
+    z0, z1 = slab_range(nglob, world, rank)
+    nz = z1 - z0
+    Mz = nz + 2 * cz
+    plane = 2 * (-(-(Mx // 2 + 1) // 16) * 16) * My
+    sl = {"fft_dims": [Mx, My, Mz], "extent": [1024, 512, nz], "kernel_planes": 2 * cz + 1,
+          "zpass_mode": zmode, "halo": halo_plan(nz, Mz, cz, plane)}
+    return {"rank": rank, "world": world, "nranks": world, "nviews": nviews, "storage_fp16": 0,
+            "fft_backend": 0, "slab_axis": 1, "nz_global": nglob, "z_offset": z0, "extent": nz,
+            "zpass_modes": [zmode], "slabs": [sl]}
+
+
+def test_rank_plans_agree_and_disagree():
+    plans = [_c3_plan(r) for r in range(8)]
+    assert check_rank_plans(plans) == []
+    bad = [dict(p) for p in plans]
+    bad[3] = _c3_plan(3, nviews=5)
+    assert any(e.startswith("nviews") for e in check_rank_plans(bad))
+    bad = [_c3_plan(r, zmode=3 if r != 5 else 1) for r in range(8)]
+    assert any(e.startswith("zpass_modes") for e in check_rank_plans(bad))
+    bad = [_c3_plan(r) for r in range(8)]
+    bad[4]["z_offset"] += 1                              # a gap between ranks 3 and 4
+    assert any("rank 3 owns" in e for e in check_rank_plans(bad))
+    bad = [_c3_plan(r, cz=12 if r != 6 else 10) for r in range(8)]   # other halo widths
+    assert any("halo transfer" in e for e in check_rank_plans(bad))
+    bad = [_c3_plan(r, My=540 if r < 7 else 576) for r in range(8)]
+    assert any("x-y spectrum planes" in e for e in check_rank_plans(bad))
+    assert check_rank_plans(plans[:7])                   # the last rank is missing
+
+
+def _plan_worker(rank, world, port, q, disagree):
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    t0 = time.perf_counter()
+    try:
+        plan = _c3_plan(rank, world=world, nglob=256, nviews=6 if (rank == 0 or not disagree) else 4)
+        verify_rank_plans(dist, plan)
+        q.put(("ok", rank, time.perf_counter() - t0))
+    except RuntimeError as e:
+        q.put(("refused", rank, time.perf_counter() - t0, str(e)))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("disagree", [False, True])
+def test_rank_plans_gloo_world2_fail_fast(disagree):
+    """world 2 over gloo: agreeing ranks both start; ranks with other view counts are both
+    refused, within seconds (no exchange is ever posted)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, 2, port, q, disagree)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in procs], key=lambda o: o[1])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kinds = {o[0] for o in out}
+    assert kinds == ({"refused"} if disagree else {"ok"}), out
+    assert all(o[2] < 30 for o in out), out
+    if disagree:
+        assert all("nviews: rank 1 has 4, rank 0 has 6" in o[3] for o in out), out

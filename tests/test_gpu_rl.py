@@ -179,6 +179,35 @@ def test_engine_pad_policies(gpu, shape, ksize, policy):
     assert rel_l2(out[0][0], res.psi) < TOL
 
 
+@pytest.mark.parametrize("fp16", [False, True])
+@pytest.mark.parametrize("psftype,lam", [(PSFTYPE.OPTIMIZATION_II, 0.0), (PSFTYPE.EFFICIENT_BAYESIAN, 0.006)])
+def test_x_tiles_2100_wave_tiles(gpu, fp16, psftype, lam):
+    """x = 2048 pads to Mx = 2100 = 42 * 50: the wave x tiles (one wave per block, one row
+    pair, no block barrier; xt_wave) in every mode -- psi spectra, quotient, plain and
+    Tikhonov update -- for f32 and fp16 storage, against the rocFFT backend and the oracle
+    (on the fp16-rounded inputs when fp16)."""
+    shape, ksize = (10, 12, 2048), (21, 3, 3)
+    imgs, ws, ks, _ = small_case(shape=shape, V=2, ksize=ksize, partial=True)
+    out = []
+    for be in ("engine", "rocfft"):
+        with Session(shape[::-1], fft_backend=be, storage_fp16=fp16) as s:
+            for i, w, k in zip(imgs, ws, ks):
+                s.add_view(i, w, k)
+            s.init(psftype)
+            s.init_psi()
+            st = s.run(3, lam)
+            s.apply_mask()
+            out.append((s.get_psi(), st, s.fft_dims(), s.xpass_mode()))
+    assert out[0][2][0] == 2100 and out[0][3] == 2, out[0][2:]
+    assert rel_l2(out[0][0], out[1][0]) < 1e-5
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-3)
+    if fp16:
+        imgs = [i.astype(np.float16).astype(np.float32) for i in imgs]
+        ws = [w.astype(np.float16).astype(np.float32) for w in ws]
+    res = ref.mv_deconvolution(imgs, ws, ks, psftype, 3, lam)
+    assert rel_l2(out[0][0], res.psi) < TOL
+
+
 def test_initial_image_and_incremental_iterations(gpu):
     imgs, ws, ks, _ = small_case(V=2)
     init = imgs[0].copy()
