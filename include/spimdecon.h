@@ -461,6 +461,12 @@ int spim_extract_psfs(int nviews, const float* const* imgs, const int64_t* dims,
                       const double* models, float* const* psf_original, float* const* psf_transformed,
                       int device);
 
+/* spim_extract_psf(s) keep one view's device buffers and stream per view between
+ * calls (a whole view when img is a host pointer, the bead samples, the PSFs); this
+ * frees them on `device` (-1: every device), e.g. before an RL session is created on
+ * the same GPU.  No reference counterpart (ExtractPSF allocates per call). */
+int spim_psf_release_workspace(int device);
+
 /* computeAverageTransformedPSF (:164-208): the PSFs (psf_dims = npsfs x 3)
  * point-mirrored about their centres and summed into the max size, written
  * to avg_dims.  avg == NULL: only the dims are returned. */

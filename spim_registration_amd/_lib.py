@@ -139,6 +139,7 @@ SIGNATURES = {
     "spim_dog_interest_points": (C.c_int, [_pf, _pi64, C.POINTER(DogParams), _pf,
                                            C.POINTER(InterestPointC), _i64, _pi64]),
     "spim_dog_release_workspace": (C.c_int, [C.c_int]),
+    "spim_psf_release_workspace": (C.c_int, [C.c_int]),
     "spim_save_interest_points": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(InterestPointC),
                                             C.POINTER(C.c_int32), C.c_int64]),
     "spim_load_interest_points": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(InterestPointC),

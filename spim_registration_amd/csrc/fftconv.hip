@@ -806,9 +806,9 @@ EngineKnobs EngineKnobs::from_env() {
     return k;
 }
 
-void SpectralPlan::create(const SlabGeom& geom, bool allow_2f, bool z_fft) {
+void SpectralPlan::create(const SlabGeom& geom, bool allow_2f, bool z_fft, const EngineKnobs& kn) {
     g = geom;
-    knobs = EngineKnobs::from_env();
+    knobs = kn;
     SD_CHECK(g.Mx % 2 == 0, SPIMDECON_ERR_ARG, "Mx must be even");
     Hx = g.Mx / 2 + 1;
     Hp = ceil_div(Hx, 16) * 16;  // column tiles of 16 (or 8/4) complex stay 128-B aligned
@@ -964,16 +964,16 @@ static ZChunk zdmc_plan(int64_t nz, int KC) {
     return best;
 }
 
-bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz) {
+bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz, bool zdirect_knob) {
     const int KC = zdirect_kc_bound(cz);
     const int64_t Hp = ceil_div(Mx / 2 + 1, int64_t(16)) * 16;
     // Mz >= KC: a chunk's window slots (plane zc - KC + s mod Mz) wrap at most once
-    return zdirect_env() && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC &&
+    return zdirect_knob && KC > 0 && Mz >= 2 * cz + 1 && Mz >= KC &&
            uint64_t(Hp) * uint64_t(My) * uint64_t(Mz) * sizeof(float2) <= kOOB;
 }
 
 bool engine_zdirect_ok(const SpectralPlan& p) {
-    return p.knobs.zdirect && p.Hp % 16 == 0 && engine_zdirect_dims_ok(p.g.Mx, p.g.My, p.g.Mz, p.g.cz);
+    return p.Hp % 16 == 0 && engine_zdirect_dims_ok(p.g.Mx, p.g.My, p.g.Mz, p.g.cz, p.knobs.zdirect);
 }
 
 int engine_zpass_mode(const SpectralPlan& p, bool compact) {

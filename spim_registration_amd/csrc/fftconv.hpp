@@ -65,7 +65,8 @@ struct SpectralPlan {
     // allow_2f: use the two-factor register kernels for lengths in the fast-path table
     // z_fft = false: no z transform plan (the direct z convolution needs none, and then
     // Mz = nz + 2 cz need not be an FFT length)
-    void create(const SlabGeom& geom, bool allow_2f, bool z_fft = true);
+    // knobs: the session's EngineKnobs, read once when its slabs are sized
+    void create(const SlabGeom& geom, bool allow_2f, bool z_fft, const EngineKnobs& knobs);
 };
 
 // FFT length for `need` samples (even when `even`).  policy 0: the two-factor
@@ -94,7 +95,7 @@ bool engine_kernel_compact_ok(const SpectralPlan& p);
 bool engine_zdirect_ok(const SpectralPlan& p);
 // the same decision from the padded dims, before a plan exists (the session then
 // sizes Mz = nz + 2 cz exactly)
-bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz);
+bool engine_zdirect_dims_ok(int64_t Mx, int64_t My, int64_t Mz, int cz, bool zdirect_knob);
 // z pass of a slab: 0 = fused FFT with full kernel spectra, 1 = fused FFT with
 // compact kernels, 3 = direct convolution with compact kernels (z chunks, k_zdmc)
 int engine_zpass_mode(const SpectralPlan& p, bool compact);

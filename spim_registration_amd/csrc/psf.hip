@@ -540,6 +540,23 @@ extern "C" int spim_extract_psfs(int nviews, const float* const* imgs, const int
     });
 }
 
+// frees the per-view buffers and streams extract_psf(s) keep on a device (-1: every device)
+void psf_release_workspace(int device) {
+    std::lock_guard<std::mutex> lk(g_psf_pool_mu);
+    for (auto& kv : g_psf_pool) {
+        if (device >= 0 && kv.first != device) continue;
+        if (!kv.second) continue;
+        std::lock_guard<std::mutex> lp(kv.second->mu);   // (no extract call in flight)
+        DeviceGuard guard(kv.first);
+        for (auto& w : kv.second->w) SD_HIP(hipStreamSynchronize(w->st.s));
+        kv.second->w.clear();
+    }
+}
+
+extern "C" int spim_psf_release_workspace(int device) {
+    return guarded([&] { psf_release_workspace(device); });
+}
+
 extern "C" int spim_average_transformed_psf(int npsfs, const float* const* psfs, const int64_t* psf_dims,
                                             float* avg, int64_t avg_dims[3], int device) {
     return guarded([&] { average_transformed_psf(npsfs, psfs, psf_dims, avg, avg_dims, device); });

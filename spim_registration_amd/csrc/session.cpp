@@ -392,6 +392,7 @@ void Session::build_spectra() {
         for (int d = 0; d < 3; ++d) h[d] = std::max(h[d], ik1[v].dims[d] / 2);
     for (int d = 0; d < 3; ++d) halo_[d] = std::max(h[d], p_.halo[d]);
     const int total_slabs = int(slabs_.size()) * p_.nranks;
+    const EngineKnobs knobs = EngineKnobs::from_env();   // read once: sizing and plans agree
     for (auto& sl : slabs_) {
         DeviceGuard guard(groups_[sl.grp].dev);
         hipStream_t stream_ = groups_[sl.grp].stream;  // this slab's device stream
@@ -412,7 +413,7 @@ void Session::build_spectra() {
         const char* zk = std::getenv("SPIMDECON_ZK");
         const bool zk_full = zk && (zk[0] == 'f' || zk[0] == 'r');
         sl.zexact = backend_ == 0 && !zk_full &&
-                    engine_zdirect_dims_ok(sl.pd.M[0], sl.pd.M[1], g.nz + 2 * g.cz, g.cz);
+                    engine_zdirect_dims_ok(sl.pd.M[0], sl.pd.M[1], g.nz + 2 * g.cz, g.cz, knobs.zdirect);
         if (sl.zexact) sl.pd.M[2] = g.nz + 2 * g.cz;
         g.Mx = sl.pd.M[0];
         g.My = sl.pd.M[1];
@@ -449,7 +450,7 @@ void Session::build_spectra() {
                 }
             }
         } else {
-            sl.sp.create(g, p_.fft_pad_policy != 2, !sl.zexact);
+            sl.sp.create(g, p_.fft_pad_policy != 2, !sl.zexact, knobs);
             const size_t ne = size_t(sl.sp.spectrum_elems());
             sl.C1.alloc(ne);
             sl.C2.alloc(ne);
@@ -884,13 +885,13 @@ void Session::run(int iters, double lambda, double* stats) {
         throw;
     }
     static const bool quiet = [] {
-        const char* e = std::getenv("SPIMDECON_VERBOSE");
+        const char* e = std::getenv("SPIMDECON_WARN_FALLBACK");
         return e && e[0] == '0';
     }();
     if (backend_ == 0 && !quiet && !warned_fallback_) {
         // the fast paths are a layout choice, not a semantic one: a slab outside them runs
         // the Stockham passes with the same results, several times slower -- say so once
-        // (SPIMDECON_VERBOSE=0 silences it; callers can query mvd_xpass_mode / mvd_zpass_mode)
+        // (SPIMDECON_WARN_FALLBACK=0 silences it; callers can query mvd_xpass_mode / mvd_zpass_mode)
         for (int s = 0; s < int(slabs_.size()); ++s) {
             const int xm = slabs_[s].sp.xmode_update, zm = zpass_mode(s);
             if (xm != 2 || zm != 3) {

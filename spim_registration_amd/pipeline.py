@@ -146,6 +146,7 @@ def process_timepoint(views, models, bb_min, bb_dims, *, psf_size=(19, 19, 25), 
     # detections rather than an all-zero PSF)
     beads = [p[c] if len(c) else p for p, c in zip(points, corr)]
     psfs = [tr for _, tr in psf_mod.extract_psfs(list(views), beads, psf_size, list(models), device=device)]
+    psf_mod.release_workspace(device)   # (the bead samples and per-view buffers: HBM the RL session can use)
     t = lap("extract_psf", t)
     sd = {}
     if digest:   # (outside the timed stages' accounting: after the lap)

@@ -111,6 +111,12 @@ def extract_psfs(imgs, locations, psf_size, models=None, device: int = 0):
     return [(origs[v], trans[v] if trans is not None else None) for v in range(n)]
 
 
+def release_workspace(device: int = -1) -> None:
+    """Frees the buffers and streams the PSF extraction keeps per view between calls
+    (spim_psf_release_workspace; -1: every device)."""
+    check(_lib.load().spim_psf_release_workspace(int(device)))
+
+
 def average_transformed_psf(psfs, device: int = 0) -> np.ndarray:
     """ExtractPSF.computeAverageTransformedPSF (:164-208)."""
     lib = _lib.load()

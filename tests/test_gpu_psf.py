@@ -109,3 +109,20 @@ def test_extract_psfs_batch_equals_per_view(gpu):
     for v in range(4):
         np.testing.assert_array_equal(host[v][0], got[v][0])
         assert host[v][1] is None
+
+
+def test_release_workspace_then_extract_again(gpu):
+    """spim_psf_release_workspace frees the per-view buffers the extraction keeps
+    between calls (on one device and on all); later calls reallocate and give the
+    same bits."""
+    img, locs = bead_view(cid=41)
+    first = psf.extract_psfs([img, img], [locs, locs[:5]], (9, 9, 11), [ROT, ROT])
+    psf.release_workspace(0)
+    again = psf.extract_psfs([img, img], [locs, locs[:5]], (9, 9, 11), [ROT, ROT])
+    psf.release_workspace()
+    single = psf.extract_psf(img, locs, (9, 9, 11), ROT)
+    for a, b in zip(first, again):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(single[1], first[0][1])
+    psf.release_workspace(0)
