@@ -151,9 +151,11 @@ typedef struct mvd_params {
     int64_t z_offset;       /* first global z plane owned by this rank             */
     int     device;         /* HIP device id (>= 0)                                */
     int     local_slabs;    /* z-slabs held by this process (>= 1); >1 = virtual shards */
-    int     nranks;         /* processes in the RCCL communicator (1 = none)       */
+    int     nranks;         /* processes in the RCCL communicator (1: none unless comm_id) */
     int     rank;
-    const char* comm_id;    /* 128-byte RCCL unique id (NULL when nranks == 1)     */
+    const char* comm_id;    /* 128-byte RCCL unique id (required when nranks > 1;
+                               with nranks == 1 a non-NULL id still makes a one-rank
+                               communicator: collectives and watchdog through RCCL) */
     int     storage_fp16;   /* 1: img/weights stored as fp16 (config-5 mode)       */
     int     fft_pad_policy; /* padded FFT length per axis (>= n + K - 1):            *
                              * 0 = auto (two-factor fast-path length when within    *

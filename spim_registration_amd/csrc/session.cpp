@@ -138,6 +138,8 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
         SD_HIP(hipStreamCreateWithFlags(&gr.xstream, hipStreamNonBlocking));
         SD_HIP(hipEventCreateWithFlags(&gr.ev_bnd, hipEventDisableTiming));
         SD_HIP(hipEventCreateWithFlags(&gr.ev_x, hipEventDisableTiming));
+        SD_HIP(hipEventCreateWithFlags(&gr.ev_pre, hipEventDisableTiming));
+        SD_HIP(hipEventCreateWithFlags(&gr.ev_bu, hipEventDisableTiming));
         // halo planes are pulled straight from the neighbours' HBM (xGMI peer access)
         for (int o : {gi - 1, gi + 1}) {
             if (o < 0 || o >= G || dl[o] == gr.dev) continue;
@@ -151,7 +153,10 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
         }
     }
     stream_ = groups_[0].stream;
-    if (p_.nranks > 1) {
+    if (const char* e = std::getenv("SPIMDECON_CBND")) cbnd_ = e[0] != '0';
+    // a communicator for several ranks -- or for one when the caller passes an id (the
+    // single-GPU tests run the collectives and the watchdog through RCCL that way)
+    if (p_.nranks > 1 || p_.comm_id != nullptr) {
         if (const char* e = std::getenv("SPIMDECON_RCCL_TIMEOUT")) rccl_timeout_s_ = std::max(1.0, std::atof(e));
         DeviceGuard guard(p_.device);
         ncclUniqueId id;
@@ -223,6 +228,8 @@ Session::~Session() {
         gr.stats.release();
         if (gr.ev_bnd) (void)hipEventDestroy(gr.ev_bnd);
         if (gr.ev_x) (void)hipEventDestroy(gr.ev_x);
+        if (gr.ev_pre) (void)hipEventDestroy(gr.ev_pre);
+        if (gr.ev_bu) (void)hipEventDestroy(gr.ev_bu);
         if (gr.xstream) (void)hipStreamDestroy(gr.xstream);
         if (gr.stream) (void)hipStreamDestroy(gr.stream);
     }
@@ -745,7 +752,7 @@ void Session::group_exchange_end(int gi) {
 }
 
 void Session::allreduce_sum(double* host, int n) {
-    if (p_.nranks == 1) return;
+    if (!comm_) return;
     DeviceGuard guard(p_.device);
     DBuf<double> d(n);
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
@@ -755,7 +762,7 @@ void Session::allreduce_sum(double* host, int n) {
 }
 
 void Session::allreduce_max(double* host, int n) {
-    if (p_.nranks == 1) return;
+    if (!comm_) return;
     DeviceGuard guard(p_.device);
     DBuf<double> d(n);
     SD_HIP(hipMemcpyAsync(d.p, host, n * 8, hipMemcpyHostToDevice, stream_));
@@ -814,7 +821,7 @@ void Session::wait_stream(hipStream_t st) {
 // the exchange geometry of this rank, all-gathered; refused on every rank when any two
 // ranks' sends and receives could not match (they would wait for each other forever)
 void Session::verify_ranks() {
-    if (p_.nranks <= 1 || !comm_) return;
+    if (!comm_) return;
     constexpr int K = 12;
     int64_t ext = 0;
     for (auto& sl : slabs_) ext += sl.g.nz;
@@ -919,7 +926,7 @@ void Session::run(int iters, double lambda, double* stats) {
             st[i + 1] = gi == 0 ? part[i + 1] : std::max(st[i + 1], part[i + 1]);
         }
     }
-    if (p_.nranks > 1) {
+    if (comm_) {
         DeviceGuard guard(p_.device);
         std::vector<double> sums(size_t(iters) * V), maxs(size_t(iters) * V);
         for (size_t i = 0; i < sums.size(); ++i) {
@@ -1050,6 +1057,16 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
         }
         if (tm && window) wstart(st);
     };
+    // (cbnd_) one group, exchange over RCCL or between its own slabs: the boundary launches
+    // were issued on xstream (after ev_pre), the exchange follows them there
+    const bool cb = cbnd_ && !bar;
+    auto TX0 = [&](int cls) { if (tm) tstart(cls, gr.xstream); };
+    auto TX1 = [&]() { if (tm) tstop(gr.xstream); };
+    auto xbegin_cb = [&](bool buffer_a) {
+        exchange(buffer_a, gr.xstream);
+        SD_HIP(hipEventRecord(gr.ev_x, gr.xstream));
+        if (tm) wstart(st);
+    };
     auto xend = [&]() {
         if (tm) wstop(st);   // (no-op after an unwindowed begin)
         if (bar) group_exchange_end(gi);
@@ -1123,7 +1140,21 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             // quotient (+ forward x of the quotient: C1 -> C2) and its halo exchange
             auto qin = [&](SlabState& sl) { return sl.C1.p; };
             auto qout = [&](SlabState& sl) { return sl.C2.p; };
-            if (overlap) {
+            if (overlap && cb) {
+                // boundary pairs on the exchange stream, the exchange right behind them there,
+                // the rest of the pass concurrently on the compute stream
+                SD_HIP(hipEventRecord(gr.ev_pre, st));
+                SD_HIP(hipStreamWaitEvent(gr.xstream, gr.ev_pre, 0));
+                for (int s = s0; s < s1; ++s) {
+                    SlabState& sl = slabs_[s];
+                    TX0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], gr.xstream); TX1();
+                }
+                xbegin_cb(false);
+                for (int s = s0; s < s1; ++s) {
+                    SlabState& sl = slabs_[s];
+                    T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), rest[s], st); T1();
+                }
+            } else if (overlap) {
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
                     T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], st); T1();
@@ -1146,15 +1177,23 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             // update (+ forward x of the next psi) and its halo exchange
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
+            const bool ovc = ov && cb;
+            if (ovc) {
+                SD_HIP(hipEventRecord(gr.ev_pre, st));
+                SD_HIP(hipStreamWaitEvent(gr.xstream, gr.ev_pre, 0));
+            }
             for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
-                T0(0);
+                if (ovc) TX0(0); else T0(0);
                 nb[s] = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
-                                      last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp), st);
-                T1();
+                                      last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp),
+                                      ovc ? gr.xstream : st);
+                if (ovc) TX1(); else T1();
             }
+            if (ovc) SD_HIP(hipEventRecord(gr.ev_bu, gr.xstream));   // the boundary partials
             if (ov) {
-                xbegin(true);
+                if (ovc) xbegin_cb(true);
+                else xbegin(true);
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
                     T0(0);
@@ -1163,6 +1202,7 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                     T1();
                 }
             }
+            if (ovc) SD_HIP(hipStreamWaitEvent(st, gr.ev_bu, 0));
             for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
                 T0(6);

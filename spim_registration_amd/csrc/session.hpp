@@ -71,6 +71,7 @@ struct DevGroup {
     hipStream_t stream = nullptr;
     hipStream_t xstream = nullptr;          // halo exchanges overlapped with the interior x pass
     hipEvent_t ev_bnd = nullptr, ev_x = nullptr;
+    hipEvent_t ev_pre = nullptr, ev_bu = nullptr;  // (boundary x launches on xstream: cbnd_)
     DBuf<double> stats;                     // iters * V * {sum, max} of this group's slabs
 };
 
@@ -187,6 +188,11 @@ private:
     // iterations, so nothing but destruction is allowed afterwards
     bool poisoned_ = false;
     bool warned_fallback_ = false;  // the Stockham-fallback warning is printed once
+    // one device group with neighbours (RCCL ranks, local slabs): the boundary x launches
+    // run on the exchange stream, concurrently with the rest of the x pass on the compute
+    // stream, and the exchange follows them there (SPIMDECON_CBND=0: both on the compute
+    // stream, the exchange after the boundary launches)
+    bool cbnd_ = true;
     std::atomic<int64_t> xbytes_{0}, xcopies_{0};  // (group threads add concurrently)
     bool timing_on_ = false;
     std::vector<TimingRec> trecs_;

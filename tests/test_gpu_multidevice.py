@@ -234,3 +234,40 @@ def test_auto_slabs_keep_the_count_when_no_split_fits(gpu):
         assert s.num_slabs() == 1
     with Session((33000, 33000, 3), devices=[0, 0], slab_axis="z") as s:
         assert s.num_slabs() == 2
+
+
+def test_single_rank_rccl_communicator(gpu, tile_ref, monkeypatch):
+    """A one-rank RCCL communicator (comm_id given with nranks = 1; the only RCCL
+    configuration one GPU admits -- two ranks cannot share a device): ncclCommInitRank,
+    the rank-geometry all-gather of Session::verify_ranks, the first-iteration and
+    per-view statistics all-reduces, and the watchdog's bounded waits on the progress
+    events all run through RCCL; psi and the statistics equal the session without a
+    communicator bit for bit (a one-rank sum / max is the identity), twice in a row."""
+    from spim_registration_amd.distributed import unique_id_bytes
+    monkeypatch.setenv("SPIMDECON_RCCL_TIMEOUT", "120")
+    imgs, ws, ks, _ = tile_case()
+    psi0, st0, _, _, _ = run_session(imgs, ws, ks)
+    for _ in range(2):
+        psi, st, modes, _, _ = run_session(imgs, ws, ks, comm_id=unique_id_bytes())
+        assert modes == [2]
+        np.testing.assert_array_equal(psi, psi0)
+        np.testing.assert_array_equal(st, st0)
+    assert rel_l2(psi, tile_ref[3]) < 1e-6
+
+
+@pytest.mark.parametrize("slabs", [2, 4])
+def test_concurrent_boundary_launches_bit_identical(gpu, tile_ref, slabs, monkeypatch):
+    """One device group with neighbouring slabs: the boundary x launches on the exchange
+    stream, concurrently with the rest of the pass (default), compute the same bits as
+    both on the compute stream (SPIMDECON_CBND=0) -- the launches write disjoint rows and
+    stats partials, and the reduction order is fixed."""
+    imgs, ws, ks, _ = tile_case()
+    out = []
+    for cb in ("0", "1"):
+        monkeypatch.setenv("SPIMDECON_CBND", cb)
+        psi, st, modes, _, _ = run_session(imgs, ws, ks, local_slabs=slabs)
+        assert modes == [2] * slabs
+        out.append((psi, st))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert rel_l2(out[1][0], tile_ref[3]) < 1e-5
