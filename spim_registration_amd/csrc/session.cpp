@@ -601,6 +601,20 @@ void Session::wstop(hipStream_t st) {
     wcur_ = -1;
 }
 
+int Session::rstart(int cls, hipStream_t st, int weight) {
+    if (!timing_on_) return -1;
+    TimingRec r{cls, get_event(), nullptr, weight};
+    SD_HIP(hipEventRecord(r.a, st));
+    trecs_.push_back(r);
+    return int(trecs_.size()) - 1;
+}
+
+void Session::rstop(int rec, hipStream_t st) {
+    if (!timing_on_ || rec < 0) return;
+    trecs_[rec].b = get_event();
+    SD_HIP(hipEventRecord(trecs_[rec].b, st));
+}
+
 void Session::timing(double* out16) {
     for (int i = 0; i < 16; ++i) out16[i] = tacc_[i];
 }
@@ -947,7 +961,7 @@ void Session::run(int iters, double lambda, double* stats) {
             float ms = 0.f;
             SD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
             tacc_[r.cls] += ms;
-            tacc_[8 + r.cls] += 1.0;
+            tacc_[8 + r.cls] += double(r.weight);
             event_pool_.push_back(r.a);
             event_pool_.push_back(r.b);
         }
@@ -1060,8 +1074,6 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
     // (cbnd_) one group, exchange over RCCL or between its own slabs: the boundary launches
     // were issued on xstream (after ev_pre), the exchange follows them there
     const bool cb = cbnd_ && !bar;
-    auto TX0 = [&](int cls) { if (tm) tstart(cls, gr.xstream); };
-    auto TX1 = [&]() { if (tm) tstop(gr.xstream); };
     auto xbegin_cb = [&](bool buffer_a) {
         exchange(buffer_a, gr.xstream);
         SD_HIP(hipEventRecord(gr.ev_x, gr.xstream));
@@ -1142,17 +1154,24 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             auto qout = [&](SlabState& sl) { return sl.C2.p; };
             if (overlap && cb) {
                 // boundary pairs on the exchange stream, the exchange right behind them there,
-                // the rest of the pass concurrently on the compute stream
+                // the rest of the pass concurrently on the compute stream; timed as one
+                // interval (compute stream, through the boundary launches' end) per pass
+                const int rq = tm ? rstart(1, st, s1 - s0) : -1;
                 SD_HIP(hipEventRecord(gr.ev_pre, st));
                 SD_HIP(hipStreamWaitEvent(gr.xstream, gr.ev_pre, 0));
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    TX0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], gr.xstream); TX1();
+                    engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), bnd[s], gr.xstream);
                 }
+                SD_HIP(hipEventRecord(gr.ev_bu, gr.xstream));
                 xbegin_cb(false);
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    T0(1); engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), rest[s], st); T1();
+                    engine_quotient(sl.sp, store_, qin(sl), sl.img[v].p, qout(sl), rest[s], st);
+                }
+                if (rq >= 0) {
+                    SD_HIP(hipStreamWaitEvent(st, gr.ev_bu, 0));   // (timing only)
+                    rstop(rq, st);
                 }
             } else if (overlap) {
                 for (int s = s0; s < s1; ++s) {
@@ -1178,17 +1197,19 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             const bool ov = overlap && !last;
             std::vector<int64_t> nb(slabs_.size(), 0);
             const bool ovc = ov && cb;
-            if (ovc) {
+            int ru = -1;
+            if (ovc) {   // (as the quotient: boundary pairs and the exchange on xstream)
+                ru = tm ? rstart(0, st, s1 - s0) : -1;
                 SD_HIP(hipEventRecord(gr.ev_pre, st));
                 SD_HIP(hipStreamWaitEvent(gr.xstream, gr.ev_pre, 0));
             }
             for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
-                if (ovc) TX0(0); else T0(0);
+                if (!ovc) T0(0);
                 nb[s] = engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
                                       last ? nullptr : sl.C1.p, sl.partials.p, ov ? bnd[s] : all_pairs(sl.sp),
                                       ovc ? gr.xstream : st);
-                if (ovc) TX1(); else T1();
+                if (!ovc) T1();
             }
             if (ovc) SD_HIP(hipEventRecord(gr.ev_bu, gr.xstream));   // the boundary partials
             if (ov) {
@@ -1196,13 +1217,16 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
                 else xbegin(true);
                 for (int s = s0; s < s1; ++s) {
                     SlabState& sl = slabs_[s];
-                    T0(0);
+                    if (!ovc) T0(0);
                     nb[s] += engine_update(sl.sp, store_, sl.C2.p, sl.psi, sl.w[v].p, lambda, sl.psi_next,
                                            sl.C1.p, sl.partials.p + 2 * nb[s], rest[s], st);
-                    T1();
+                    if (!ovc) T1();
                 }
             }
-            if (ovc) SD_HIP(hipStreamWaitEvent(st, gr.ev_bu, 0));
+            if (ovc) {
+                SD_HIP(hipStreamWaitEvent(st, gr.ev_bu, 0));
+                rstop(ru, st);
+            }
             for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
                 T0(6);

@@ -62,6 +62,7 @@ struct SlabState {
 struct TimingRec {
     int cls;
     hipEvent_t a, b;
+    int weight = 1;   // whole-slab passes the interval covers (counted into the class)
 };
 
 // one device of a multi-device session (or the only one)
@@ -167,6 +168,10 @@ private:
     // between the exchange's start and the wait for it (group 0's stream)
     void wstart(hipStream_t st);
     void wstop(hipStream_t st);
+    // an interval of class cls covering `weight` whole-slab passes, independent of tcur_
+    // (the concurrent boundary / rest x launches: one interval across both streams)
+    int rstart(int cls, hipStream_t st, int weight);
+    void rstop(int rec, hipStream_t st);
     int wcur_ = -1;
 
     mvd_params p_{};        // internal geometry (dims / halo with y and z swapped when axis_ == 1)
