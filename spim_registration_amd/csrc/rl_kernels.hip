@@ -459,6 +459,34 @@ void launch_next_value(const float* last, const float* integral, const float* we
     SD_HIP(hipGetLastError());
 }
 
+// halo planes pulled by a kernel (SPIMDECON_PULL=kernel) instead of hipMemcpyAsync: the
+// loads read the source's HBM directly (a peer device's over xGMI when src lives there,
+// peer access enabled), 16-B accesses, four in flight per lane, a few blocks only
+__global__ __launch_bounds__(256) void k_pull_copy(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                   int64_t n4) {
+    const int64_t stride = int64_t(gridDim.x) * 256;
+    int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+void launch_pull_copy(float* dst, const float* src, size_t bytes, hipStream_t s) {
+    SD_CHECK(bytes % 16 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0,
+             SPIMDECON_ERR_ARG, "pull copy needs 16-B aligned whole float4");
+    const int64_t n4 = int64_t(bytes / 16);
+    if (n4 == 0) return;
+    const unsigned grid = unsigned(std::min<int64_t>(64, (n4 + 1023) / 1024));
+    hipLaunchKernelGGL(k_pull_copy, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
+                       reinterpret_cast<float4*>(dst), n4);
+    SD_HIP(hipGetLastError());
+}
+
 void launch_to_half(const float* in, void* out, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_to_half, dim3(grid_for(n, 256)), dim3(256), 0, s, in,
                        static_cast<__half*>(out), n);

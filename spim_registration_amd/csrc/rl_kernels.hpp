@@ -63,6 +63,8 @@ void launch_mask(float* psi, int64_t n, int nviews, Store st, const void* const*
                  hipStream_t s);
 // float32 -> fp16 conversion (storage mode)
 void launch_to_half(const float* in, void* out, int64_t n, hipStream_t s);
+// bytes from src to dst by a copy kernel on s (src may live on a peer device)
+void launch_pull_copy(float* dst, const float* src, size_t bytes, hipStream_t s);
 // Swaps the two outer axes of an x-fastest volume, whole x rows at a time (the
 // y-slab layout of the session): a [nz][ny][nx] -> b[ny][nz][nx], b(y,z) = a(z,y).
 // Coalesced row copies (one block per row pair of 4 rows), nx % 4 == 0 not needed.

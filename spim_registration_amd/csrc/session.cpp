@@ -154,6 +154,7 @@ Session::Session(const mvd_params& p0, const std::vector<int>& devs) {
     }
     stream_ = groups_[0].stream;
     if (const char* e = std::getenv("SPIMDECON_CBND")) cbnd_ = e[0] != '0';
+    if (const char* e = std::getenv("SPIMDECON_PULL")) pull_kernel_ = e[0] == 'k';
     // a communicator for several ranks -- or for one when the caller passes an id (the
     // single-GPU tests run the collectives and the watchdog through RCCL that way)
     if (p_.nranks > 1 || p_.comm_id != nullptr) {
@@ -682,9 +683,9 @@ void Session::exchange(bool which, hipStream_t st) {
         SlabState& hi = slabs_[s];
         const HaloPlan hl = hp(lo), hh = hp(hi);
         // hi's first cz planes -> lo's upper halo
-        SD_HIP(hipMemcpyAsync(get(lo) + hl.recv_hi, get(hi) + hh.send_lo, bytes, hipMemcpyDeviceToDevice, st));
+        copy_halo(get(lo) + hl.recv_hi, get(hi) + hh.send_lo, bytes, st, false);
         // lo's last cz planes -> hi's lower halo
-        SD_HIP(hipMemcpyAsync(get(hi) + hh.recv_lo, get(lo) + hl.send_hi, bytes, hipMemcpyDeviceToDevice, st));
+        copy_halo(get(hi) + hh.recv_lo, get(lo) + hl.send_hi, bytes, st, false);
     }
     xbytes_ += int64_t(2) * (S - 1) * int64_t(bytes);
     xcopies_ += int64_t(2) * (S - 1);
@@ -709,6 +710,15 @@ void Session::exchange(bool which, hipStream_t st) {
         xcopies_ += nsend;
     }
     tstop(st);
+}
+
+// One halo transfer between slabs of this process.  hipMemcpyAsync: between two GPUs a
+// peer copy (ROCm runs it on an SDMA engine unless HSA_ENABLE_SDMA=0), on one GPU a blit
+// kernel; SPIMDECON_PULL=kernel: k_pull_copy on the receiving device's stream, whose
+// loads read the sender's HBM over xGMI (peer access is enabled between neighbours).
+void Session::copy_halo(float* dst, const float* src, size_t bytes, hipStream_t st, bool peer) {
+    if (pull_kernel_) launch_pull_copy(dst, src, bytes, st);
+    else SD_HIP(hipMemcpyAsync(dst, src, bytes, peer ? hipMemcpyDefault : hipMemcpyDeviceToDevice, st));
 }
 
 // Multi-device exchange, run by every group thread at the same point of the schedule.
@@ -737,16 +747,14 @@ void Session::group_exchange_begin(int gi, bool which, HostBarrier& bar) {
             if (s > 0) {  // lower neighbour's last cz planes -> my lower halo
                 SlabState& lo = slabs_[s - 1];
                 const HaloPlan hl = halo_plan(lo.g.nz, lo.g.Mz, cz, plane);
-                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + hm.recv_lo,
-                                      buf_ptr(lo, which, backend_) + hl.send_hi, bytes, hipMemcpyDefault,
-                                      gr.xstream));
+                copy_halo(buf_ptr(me, which, backend_) + hm.recv_lo, buf_ptr(lo, which, backend_) + hl.send_hi,
+                          bytes, gr.xstream, true);
             }
             if (s < S - 1) {  // upper neighbour's first cz planes -> my upper halo
                 SlabState& hi = slabs_[s + 1];
                 const HaloPlan hh = halo_plan(hi.g.nz, hi.g.Mz, cz, plane);
-                SD_HIP(hipMemcpyAsync(buf_ptr(me, which, backend_) + hm.recv_hi,
-                                      buf_ptr(hi, which, backend_) + hh.send_lo, bytes, hipMemcpyDefault,
-                                      gr.xstream));
+                copy_halo(buf_ptr(me, which, backend_) + hm.recv_hi, buf_ptr(hi, which, backend_) + hh.send_lo,
+                          bytes, gr.xstream, true);
             }
             const int npull = (s > 0 ? 1 : 0) + (s < S - 1 ? 1 : 0);
             xbytes_ += int64_t(npull) * int64_t(bytes);

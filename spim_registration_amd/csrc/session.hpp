@@ -198,6 +198,10 @@ private:
     // stream, and the exchange follows them there (SPIMDECON_CBND=0: both on the compute
     // stream, the exchange after the boundary launches)
     bool cbnd_ = true;
+    // halo copies between slabs of this process (local slabs, device-group peer pulls) by
+    // a copy kernel instead of hipMemcpyAsync (SPIMDECON_PULL=kernel); RCCL is unaffected
+    bool pull_kernel_ = false;
+    void copy_halo(float* dst, const float* src, size_t bytes, hipStream_t st, bool peer);
     std::atomic<int64_t> xbytes_{0}, xcopies_{0};  // (group threads add concurrently)
     bool timing_on_ = false;
     std::vector<TimingRec> trecs_;

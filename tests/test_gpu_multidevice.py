@@ -271,3 +271,18 @@ def test_concurrent_boundary_launches_bit_identical(gpu, tile_ref, slabs, monkey
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
     assert rel_l2(out[1][0], tile_ref[3]) < 1e-5
+
+
+@pytest.mark.parametrize("kw", [dict(devices=[0, 0], local_slabs=2), dict(local_slabs=3)])
+def test_kernel_pull_bit_identical(gpu, kw, monkeypatch):
+    """Halo planes moved by the pull kernel (SPIMDECON_PULL=kernel: k_pull_copy reads the
+    sender's buffer) instead of hipMemcpyAsync -- device-group pulls and local slab copies
+    -- give the same bits."""
+    imgs, ws, ks, _ = tile_case()
+    out = []
+    for pull in ("copy", "kernel"):
+        monkeypatch.setenv("SPIMDECON_PULL", pull)
+        psi, st, _, _, _ = run_session(imgs, ws, ks, **kw)
+        out.append((psi, st))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
