@@ -531,27 +531,17 @@ unsigned launch_xtile(const XArgs& a, Store st, const SpectralPlan& p, hipStream
     const int NP = xt_np(MODE, L);
     const size_t lds = xt_lds(L, NP, xt_twg(L, NP));
     if (lds > 160 * 1024) return 0;
-    unsigned grid = unsigned(std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(NP))));
+    const unsigned grid = unsigned(std::max<int64_t>(1, ceil_div(int64_t(a.pn0) + a.pn1, int64_t(NP))));
     const int sv = st == Store::F32 ? 0 : 1;
     bool done = false;
     const bool tik = MODE == XM_UPDATE && a.lambda > 0.0;
 #define SD_XT(SV, A, B, TK)                                                                                \
     if (!done && sv == SV && L == (A) * (B) && tik == TK) {                                               \
         constexpr int TRv = SD_2F_TR(A, B);                                                               \
-        constexpr bool PFv = xt_pf((A) * (B)) && MODE != XM_PSI;                                          \
         constexpr int NPv = xt_np(MODE, (A) * (B));                                                       \
-        auto kfn = &k_xtile<MODE, SV, A, B, TK, NPv, TRv, PFv>;                                           \
+        auto kfn = &k_xtile<MODE, SV, A, B, TK, NPv, TRv>;                                                \
         SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                    int(lds)));                                                            \
-        if constexpr (PFv) {   /* persistent: the resident blocks stride over the tiles */              \
-            static const int per_cu = [&] {                                                               \
-                int n = 1;                                                                                \
-                SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kfn), \
-                                                                    NPv * TRv, lds));                     \
-                return std::max(1, n);                                                                    \
-            }();                                                                                          \
-            grid = unsigned(std::min<int64_t>(grid, int64_t(256) * per_cu));                              \
-        }                                                                                                 \
         hipLaunchKernelGGL(kfn, dim3(grid), dim3(NPv * TRv), lds, s, b);                                  \
         done = true;                                                                                      \
     }
