@@ -7,6 +7,8 @@
 //   computeQuotient         spim/process/fusion/deconvolution/MVDeconvolution.java:473-525
 //   computeFinalValues      spim/process/fusion/deconvolution/MVDeconvolution.java:582-705
 #include "fftconv.hpp"
+
+#include <climits>
 #include "rl_math.hpp"
 
 #include <cmath>
@@ -647,7 +649,7 @@ constexpr int kColGridRounds = 16;
 // MODE 5: K is the compact kernel (2*kc+1 z-planes, engine_kernel_compact).
 template <int AXIS, int MODE>
 bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2* K, hipStream_t s,
-                  int tx0 = 0, int ntxb = -1, int kc = 0, int nout = -1) {
+                  int tx0 = 0, int ntxb = -1, int kc = 0, int nout = -1, int zsplit = INT_MAX, int zskip = 0) {
     // nout: z planes the pass must produce (AXIS 1: planes transformed; AXIS 2 fused
     // modes: planes stored) -- the RL loop only reads the nz interior planes back
     if (nout < 0) nout = int(p.g.Mz);
@@ -691,7 +693,8 @@ bool launch_col2f(const SpectralPlan& p, const Fft1D& f, float2* C, const float2
             SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col2f<AXIS, A, B, MODE, T, TRv, PFV>), \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));                  \
             hipLaunchKernelGGL((k_col2f<AXIS, A, B, MODE, T, TRv, PFV>), dim3(grid), dim3(T * TRv), lds, s,     \
-                               p.g, p.Hp, f.tw, C, K, rbytes, tx0, ntxb, kc, uint32_t(kbytes), nout);         \
+                               p.g, p.Hp, f.tw, C, K, rbytes, tx0, ntxb, kc, uint32_t(kbytes), nout, zsplit,  \
+                               zskip);                                                                       \
             done = true;
 #define SD_2F_C1(A, B, T)                                                                                  \
     if constexpr (MODE < 2 || SD_2F_TR(A, B) == 32) {                                                      \
@@ -1020,6 +1023,14 @@ void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s) {
     // the inverse feeds the x passes, which read the nz interior planes only
     if (inv) launch_col<1, true, 0>(p, p.fy, C, nullptr, s, int(p.g.nz));
     else launch_col<1, false, 0>(p, p.fy, C, nullptr, s);
+}
+
+bool engine_ypass_planes2(const SpectralPlan& p, float2* C, int z0, int z1, int z2, int z3, hipStream_t s) {
+    if (!p.fy.n1 || z0 < 0 || z1 < z0 || z2 < z1 || z3 < z2 || z3 > int(p.g.Mz)) return false;
+    if (z3 - z2 + z1 - z0 <= 0) return true;
+    // planes [z0, z1) and [z2, z3) in one launch: tile rows past z1 - z0 skip z2 - z1 planes
+    return launch_col2f<1, 0>(p, p.fy, C + size_t(z0) * size_t(p.g.My) * size_t(p.Hp), nullptr, s, 0, -1, 0,
+                              (z1 - z0) + (z3 - z2), z1 - z0, z2 - z1);
 }
 
 bool engine_ypass_planes(const SpectralPlan& p, float2* C, int z0, int z1, hipStream_t s) {

@@ -108,6 +108,8 @@ void engine_ypass(const SpectralPlan& p, float2* C, bool inv, hipStream_t s);
 // Forward y pass of the z planes [z0, z1) only (false: not available for this plan,
 // run engine_ypass instead)
 bool engine_ypass_planes(const SpectralPlan& p, float2* C, int z0, int z1, hipStream_t s);
+// the same over [z0, z1) and [z2, z3) as one launch
+bool engine_ypass_planes2(const SpectralPlan& p, float2* C, int z0, int z1, int z2, int z3, hipStream_t s);
 // Z pass: forward z FFT, multiply by K (when K != nullptr) and inverse z FFT
 void engine_zpass(const SpectralPlan& p, float2* C, const float2* K, hipStream_t s);
 // packed row pairs (rows 2i, 2i+1 of the My*Mz padded rows) an x pass covers:

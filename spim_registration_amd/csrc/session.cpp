@@ -1133,8 +1133,10 @@ void Session::run_engine(int gi, int iters, double lambda, HostBarrier* bar) {
             for (int s = s0; s < s1; ++s) {
                 SlabState& sl = slabs_[s];
                 T0(2);
-                SD_CHECK(engine_ypass_planes(sl.sp, buf(sl), 0, czx, st) &&
-                             engine_ypass_planes(sl.sp, buf(sl), int(sl.g.nz) - czx, int(sl.g.Mz), st),
+                // the planes that waited, [0, cz) and [nz - cz, Mz), in one launch (two small
+                // launches ran two partial rounds: C3 as 8 slabs +0.5 %, bit-identical;
+                // profiles/r06_ymerge_ab.txt)
+                SD_CHECK(engine_ypass_planes2(sl.sp, buf(sl), 0, czx, int(sl.g.nz) - czx, int(sl.g.Mz), st),
                          SPIMDECON_ERR_STATE, "y pass of a plane range not available");
                 T1();
             }
