@@ -794,7 +794,9 @@ void Session::allreduce_max(double* host, int n) {
 }
 
 void Session::record_progress(hipStream_t st) {
-    if (!comm_) return;
+    // (one device group: with several, run_engine runs on a thread per group and only the
+    // RCCL-free device-group exchange is used)
+    if (!comm_ || groups_.size() > 1) return;
     if (nprogress_ == progress_.size()) {
         hipEvent_t e;
         SD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
