@@ -480,6 +480,45 @@ int spim_average_transformed_psf(int npsfs, const float* const* psfs, const int6
 int spim_max_projection(const float* img, const int64_t dims[3], int min_dim, float* out, int64_t out_dims[2],
                         int* used_dim, int device);
 
+/* ======================================================================
+ * 10. Legacy simultaneous-update multiview RL (opt-in) --
+ *     mpicbg/spim/postprocessing/deconvolution/LucyRichardsonMultiViewDeconvolution.java
+ *     :24-358 (lucyRichardsonMultiView; LucyRichardsonFFT.java:7-38 holds one view).
+ *     Every view's correction is computed from the same psi (not MVDeconvolution's
+ *     sequential rule, section 5), so the views shard over ranks -- view v on rank
+ *     v % nranks, as the reference hands view v to thread v % numThreads (:127-128) --
+ *     and the per-voxel merge of the corrections is one RCCL all-reduce of a double
+ *     per voxel each iteration (a product when multiplicative, else a sum).  Every
+ *     rank holds the whole psi; all ranks return the same psi and statistics.
+ *     The convolutions extend their input by mirroring (extendMirrorSingle): the
+ *     reference's imglib1 FourierConvolution is absent and its extension not restated.
+ * ====================================================================== */
+typedef struct lrsim_session lrsim_session;
+
+/* dims {nx, ny, nz} of the whole volume; nranks > 1 needs the 128-byte comm_id of
+ * mvd_comm_unique_id (a non-NULL id with nranks == 1 makes a one-rank communicator) */
+int  lrsim_create(const int64_t* dims, int device, int nranks, int rank, const char* comm_id,
+                  lrsim_session** out);
+void lrsim_destroy(lrsim_session* h);
+/* Adds view number <views so far> (the data list order of the reference).  Every rank
+ * adds every view; kdims (odd {kx, ky, kz}) is always required, img / weight / kernel
+ * (raw PSF; normImage'd at init) only for the views this rank owns -- NULL otherwise.
+ * img / weight: dims voxels, host or device pointers.  Weights are required: the
+ * reference's normAllImages reads one per view (:401). */
+int  lrsim_add_view(lrsim_session* h, const float* img, const float* weight, const float* kernel,
+                    const int* kdims);
+int  lrsim_owns_view(lrsim_session* h, int view, int* owned);
+/* normImage of every kernel (:45-58, exact sum as BigDecimal), psi = (float) the
+ * average intensity where two or more views overlap (normAllImages :360-457) */
+int  lrsim_init(lrsim_session* h, double* avg_out);
+/* iters iterations (the reference's do-while runs max(1, maxIterations)); stats (may be
+ * NULL): iters x {sumChange, maxChange} (:309-330).  lambda > 0: Tikhonov (:290-301). */
+int  lrsim_run(lrsim_session* h, int iters, int multiplicative, double lambda, double* stats);
+/* psi (dims voxels) into a host or device buffer */
+int  lrsim_get_psi(lrsim_session* h, float* out);
+/* padded FFT lengths {Mx, My, Mz} (info) */
+int  lrsim_fft_dims(lrsim_session* h, int64_t* out3);
+
 #ifdef __cplusplus
 }
 #endif

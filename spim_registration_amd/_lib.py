@@ -159,6 +159,14 @@ SIGNATURES = {
     "spim_max_projection": (C.c_int, [_pf, _pi64, C.c_int, _pf, _pi64, C.POINTER(C.c_int), C.c_int]),
     "spim_fuse_weighted_average": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(FusionParams),
                                              _pf, _pf, _pf]),
+    "lrsim_create": (C.c_int, [_pi64, C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "lrsim_destroy": (None, [C.c_void_p]),
+    "lrsim_add_view": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, _pi]),
+    "lrsim_owns_view": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "lrsim_init": (C.c_int, [C.c_void_p, _pd]),
+    "lrsim_run": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, _pd]),
+    "lrsim_get_psi": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "lrsim_fft_dims": (C.c_int, [C.c_void_p, _pi64]),
     "spim_prepare_inputs": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(InputParams),
                                       C.POINTER(_pf), C.POINTER(_pf), C.POINTER(C.c_double),
                                       C.POINTER(C.c_int), C.POINTER(C.c_double)]),
