@@ -77,6 +77,9 @@ def parse(argv=None):
     ap.add_argument("--no-strong-line", action="store_true",
                     help="skip the extra strong-scaling C3 measurement (the 'strong' key)")
     ap.add_argument("--strong-steps", type=int, default=4)
+    ap.add_argument("--no-legacy-line", action="store_true",
+                    help="skip the opt-in legacy simultaneous-update line (lrsim_*: one view per GPU, "
+                         "the compound-correction all-reduce over the ranks)")
     ap.add_argument("--allow-fallback", action="store_true",
                     help="measure even when a slab runs outside the fast engine passes (else rc != 0)")
     ap.add_argument("--no-default-mode", action="store_true",
@@ -297,6 +300,59 @@ def slab_geom(sess, nslabs, ngpus):
             "nz_int": ext[2], "Mz": M[2], "kplanes": sess.kernel_planes(0), "nslabs": nslabs, "ngpus": ngpus}
 
 
+def legacy_line(args, rank, world, local, dist, broadcast_comm_id, barrier, max_over_ranks, edge=512, iters=3):
+    """LucyRichardsonMultiViewDeconvolution (:24-358) through lrsim_*: V = world views of
+    edge^3 (view v on rank v % world, generated from its own seed on the rank that owns it),
+    25^3 PSFs, additive rule, lambda 0.006; Mvoxels/s of the volume per iteration, max over
+    ranks, after one warm-up iteration."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from spim_registration_amd import _lib, synthetic
+    lib = _lib.load()
+    V = max(1, world)
+    os.environ.setdefault("SPIMDECON_RCCL_TIMEOUT", "120")   # (read when the session is created)
+    comm_id = broadcast_comm_id(dist, rank) if world > 1 else None
+    d = (C.c_int64 * 3)(edge, edge, edge)
+    h = C.c_void_p()
+    cid = None if comm_id is None else C.create_string_buffer(bytes(comm_id), 128)
+    _lib.check(lib.lrsim_create(d, local, world, rank, cid, C.byref(h)))
+    keep = []
+    try:
+        kd = np.array([25, 25, 25], np.int32)
+        for v in range(V):
+            k = synthetic.psf(v, V, (25, 25, 25))
+            keep.append(k)
+            if v % world == rank:
+                g = torch.Generator(device=f"cuda:{local}").manual_seed(1000 + v)
+                img = torch.rand((edge,) * 3, device=f"cuda:{local}", generator=g) + 0.1
+                w = torch.rand((edge,) * 3, device=f"cuda:{local}", generator=g)
+                torch.cuda.synchronize()
+                _lib.check(lib.lrsim_add_view(h, img.data_ptr(), w.data_ptr(), k.ctypes.data,
+                                              kd.ctypes.data_as(_lib._pi)))
+                del img, w
+            else:
+                _lib.check(lib.lrsim_add_view(h, None, None, None, kd.ctypes.data_as(_lib._pi)))
+        _lib.check(lib.lrsim_init(h, None))
+        _lib.check(lib.lrsim_run(h, 1, 0, 0.006, None))
+        barrier()
+        t0 = time.perf_counter()
+        _lib.check(lib.lrsim_run(h, iters, 0, 0.006, None))
+        t = time.perf_counter() - t0
+        barrier()
+        t = max_over_ranks(t)
+    finally:
+        lib.lrsim_destroy(h)
+    return {"workload": f"{V}-view {edge}^3 (one view per GPU), 25^3 PSF, additive rule, lambda=0.006: "
+                        "LucyRichardsonMultiViewDeconvolution via lrsim_* (opt-in; not the headline rule)",
+            "value": round(edge ** 3 * iters / t / 1e6, 1), "unit": "Mvoxels/s per iteration",
+            "ms_per_step": round(t / iters * 1e3, 3), "views": V, "ranks": world,
+            "allreduce": ("ncclAllReduce (sum) of 8 B per voxel per iteration" if world > 1 else
+                          "none (one rank)")}
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -460,6 +516,17 @@ def main(argv=None):
                       "fft_dims_xyz_slab0_internal": list(s3.fft_dims(0))}
         torch.cuda.empty_cache()
 
+    # ---- the opt-in legacy simultaneous update (lrsim_*): one 512^3 view per GPU, the views
+    # sharded over the ranks and one all-reduce of a double per voxel per iteration -- on the
+    # 8-GPU node the first data-path RCCL all-reduce; reported beside the headline, never as it
+    legacy = None
+    if not args.no_legacy_line and (mode == "ranks" or N == 1):
+        try:
+            legacy = legacy_line(args, rank, world, local, dist, broadcast_comm_id, barrier, max_over_ranks)
+        except Exception as e:   # (a failure here must not cost the headline line)
+            legacy = {"error": repr(e)[:400]}
+        torch.cuda.empty_cache()
+
     cpu = None
     if rank == 0 and N == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -499,6 +566,7 @@ def main(argv=None):
             "pointwise": head.get("pointwise"),
             "kernel_ms": head.get("kernel_ms"),
             "strong": strong,
+            "legacy_simultaneous": legacy,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

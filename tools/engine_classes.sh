@@ -14,7 +14,7 @@ declare -A CFG=(
   [c5]="--c5-rank --steps 4 --warmup 1"
 )
 for n in headline c3 c3x8 c4 c5; do
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline ${CFG[$n]} > $OUT/$n.log 2>&1 || { echo "$n failed"; tail -5 $OUT/$n.log; exit 1; }
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-legacy-line ${CFG[$n]} > $OUT/$n.log 2>&1 || { echo "$n failed"; tail -5 $OUT/$n.log; exit 1; }
   tail -1 $OUT/$n.log > $OUT/$n.json
   python3 - $OUT/$n.json $n <<'PY'
 import json, sys

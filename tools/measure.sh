@@ -6,7 +6,7 @@ OUT=$1
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python3 bench.py > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.log > $OUT/bench.json &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o k --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-strong-line > $OUT/kt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o k --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-strong-line --no-legacy-line > $OUT/kt.log 2>&1 &&
 cp $(ls $OUT/kt/*/k_kernel_stats.csv $OUT/kt/k_kernel_stats.csv 2>/dev/null | head -1) $OUT/kernel_stats.csv &&
 tools/pmc_engine.sh $OUT/pmc &&
 DIMS=$(python3 -c "import json; print(','.join(map(str, json.load(open('$OUT/bench.json'))['config']['fft_dims_xyz'])))") &&
