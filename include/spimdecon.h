@@ -499,6 +499,11 @@ typedef struct lrsim_session lrsim_session;
  * mvd_comm_unique_id (a non-NULL id with nranks == 1 makes a one-rank communicator) */
 int  lrsim_create(const int64_t* dims, int device, int nranks, int rank, const char* comm_id,
                   lrsim_session** out);
+/* One process, several GPUs (the reference's threads, LRMV:118-178): view v goes to
+ * devs[v % ndev] (ids may repeat); each device holds a psi replica and its views' partial,
+ * merged on devs[0] over xGMI each iteration (a sum or a product, in device order), and
+ * the new psi copied back.  No RCCL. */
+int  lrsim_create_devices(const int64_t* dims, const int* devs, int ndev, lrsim_session** out);
 void lrsim_destroy(lrsim_session* h);
 /* Adds view number <views so far> (the data list order of the reference).  Every rank
  * adds every view; kdims (odd {kx, ky, kz}) is always required, img / weight / kernel
@@ -508,6 +513,8 @@ void lrsim_destroy(lrsim_session* h);
 int  lrsim_add_view(lrsim_session* h, const float* img, const float* weight, const float* kernel,
                     const int* kdims);
 int  lrsim_owns_view(lrsim_session* h, int view, int* owned);
+/* device holding view `view` on this rank (-1: another rank's view) */
+int  lrsim_view_device(lrsim_session* h, int view, int* device);
 /* normImage of every kernel (:45-58, exact sum as BigDecimal), psi = (float) the
  * average intensity where two or more views overlap (normAllImages :360-457) */
 int  lrsim_init(lrsim_session* h, double* avg_out);

@@ -160,7 +160,9 @@ SIGNATURES = {
     "spim_fuse_weighted_average": (C.c_int, [C.c_int, C.POINTER(ViewSource), C.POINTER(FusionParams),
                                              _pf, _pf, _pf]),
     "lrsim_create": (C.c_int, [_pi64, C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "lrsim_create_devices": (C.c_int, [_pi64, _pi, C.c_int, C.POINTER(C.c_void_p)]),
     "lrsim_destroy": (None, [C.c_void_p]),
+    "lrsim_view_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "lrsim_add_view": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, _pi]),
     "lrsim_owns_view": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "lrsim_init": (C.c_int, [C.c_void_p, _pd]),

@@ -300,33 +300,75 @@ __global__ __launch_bounds__(1024) void k_lr_sum2(const double* __restrict__ par
     }
 }
 
+// a = a + b, or a * b (mult): one device group's partial merged into group 0's
+__global__ __launch_bounds__(kB) void k_lr_merge(double* __restrict__ a, const double* __restrict__ b, int64_t n,
+                                                 int mult) {
+    for (int64_t i = int64_t(blockIdx.x) * kB + threadIdx.x; i < n; i += int64_t(gridDim.x) * kB)
+        a[i] = mult ? a[i] * b[i] : a[i] + b[i];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- the session
 
 struct LrView {
     int kd[3] = {0, 0, 0};         // {kx, ky, kz}
-    bool own = false;
+    int grp = -1;                  // device group holding the view (-1: another rank's view)
     std::vector<float> kernel;     // normalised at init (LRMV:45-58)
-    DBuf<float> img, w, spec;      // owned views only
+    DBuf<float> img, w, spec;      // held views only
+};
+
+// One device's replica: psi, the padded buffers, its views' partial value.  Group 0 also
+// merges the other groups' partials, applies the rule and hands psi back to them.
+struct LrGroup {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;
+    FftPlan3D plan;
+    DBuf<float> psi, Ra, Rb, Rc;
+    DBuf<double> value, num, tmp;  // tmp (group 0): another group's partial, merged from there
+    DBuf<const float*> ptrs;       // the group's img pointers, then its weight pointers
+    int nown = 0;
 };
 
 class LrSim {
 public:
-    LrSim(const int64_t* dims, int device, int nranks, int rank, const char* comm_id) {
+    // devs: the device of each group (repeats allowed: several groups on one GPU run the
+    // same code path); views go to groups round robin, as the reference's threads take them
+    LrSim(const int64_t* dims, const std::vector<int>& devs, int nranks, int rank, const char* comm_id) {
         SD_CHECK(dims && dims[0] >= 1 && dims[1] >= 1 && dims[2] >= 1, SPIMDECON_ERR_ARG, "bad dims");
         SD_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, SPIMDECON_ERR_ARG, "bad rank");
         SD_CHECK(nranks == 1 || comm_id != nullptr, SPIMDECON_ERR_ARG, "nranks > 1 needs comm_id");
-        check_device(device);
+        SD_CHECK(!devs.empty(), SPIMDECON_ERR_ARG, "no devices");
+        SD_CHECK(devs.size() == 1 || (nranks == 1 && comm_id == nullptr), SPIMDECON_ERR_ARG,
+                 "several devices per process and RCCL ranks cannot be combined");
+        for (int d : devs) check_device(d);
         for (int d = 0; d < 3; ++d) dims_[d] = dims[d];
         n_ = dims[0] * dims[1] * dims[2];
-        dev_ = device;
         nranks_ = nranks;
         rank_ = rank;
-        DeviceGuard guard(dev_);
-        SD_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+        grp_ = std::vector<LrGroup>(devs.size());   // (LrGroup is not movable: sized once)
+        for (size_t g = 0; g < devs.size(); ++g) {
+            LrGroup& G = grp_[g];
+            G.dev = devs[g];
+            DeviceGuard guard(G.dev);
+            SD_HIP(hipStreamCreateWithFlags(&G.st, hipStreamNonBlocking));
+            SD_HIP(hipEventCreateWithFlags(&G.ev, hipEventDisableTiming));
+            if (g > 0 && G.dev != devs[0]) {   // partials and psi move between group 0 and g over xGMI
+                for (auto pr : {std::make_pair(G.dev, devs[0]), std::make_pair(devs[0], G.dev)}) {
+                    int can = 0;
+                    SD_HIP(hipDeviceCanAccessPeer(&can, pr.first, pr.second));
+                    if (!can) continue;
+                    DeviceGuard g2(pr.first);
+                    const hipError_t e = hipDeviceEnablePeerAccess(pr.second, 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) SD_HIP(e);
+                    (void)hipGetLastError();
+                }
+            }
+        }
         if (comm_id) {
             if (const char* e = std::getenv("SPIMDECON_RCCL_TIMEOUT")) timeout_s_ = std::max(1.0, std::atof(e));
+            DeviceGuard guard(grp_[0].dev);
             ncclUniqueId id;
             std::memcpy(&id, comm_id, sizeof(id));
             SD_NCCL_LR(ncclCommInitRank(&comm_, nranks, id, rank));
@@ -334,17 +376,33 @@ public:
     }
 
     ~LrSim() {
-        DeviceGuard guard(dev_);
-        if (!dead_ && st_) (void)hipStreamSynchronize(st_);
-        if (comm_) ncclCommDestroy(comm_);
+        if (comm_) {
+            DeviceGuard guard(grp_[0].dev);
+            ncclCommDestroy(comm_);
+        }
         if (dead_) {   // an aborted communicator: do not block in hipFree behind dead work
             new std::vector<LrView>(std::move(views_));
+            new std::vector<LrGroup>(std::move(grp_));
             return;
         }
-        views_.clear();
-        psi_.release(); Ra_.release(); Rb_.release(); Rc_.release();
-        value_.release(); num_.release(); part_.release(); red_.release(); ptrs_.release();
-        if (st_) (void)hipStreamDestroy(st_);
+        for (auto& G : grp_) {
+            DeviceGuard guard(G.dev);
+            if (G.st) (void)hipStreamSynchronize(G.st);
+        }
+        for (auto& v : views_) {
+            if (v.grp < 0) continue;
+            DeviceGuard guard(grp_[v.grp].dev);
+            v.img.release(); v.w.release(); v.spec.release();
+        }
+        for (auto& G : grp_) {
+            DeviceGuard guard(G.dev);
+            G.psi.release(); G.Ra.release(); G.Rb.release(); G.Rc.release();
+            G.value.release(); G.num.release(); G.tmp.release(); G.ptrs.release();
+            if (G.ev) (void)hipEventDestroy(G.ev);
+            if (G.st) (void)hipStreamDestroy(G.st);
+        }
+        part_.release();
+        red_.release();
     }
 
     void add_view(const float* img, const float* w, const float* kernel, const int* kd) {
@@ -354,16 +412,19 @@ public:
             SD_CHECK(kd[d] % 2 == 1, SPIMDECON_ERR_ARG, "kernel dims must be odd");
         LrView v;
         for (int d = 0; d < 3; ++d) v.kd[d] = kd[d];
-        v.own = int(views_.size()) % nranks_ == rank_;   // LRMV:127-128, threads -> ranks
-        if (v.own) {
+        const int idx = int(views_.size());
+        if (idx % nranks_ == rank_)   // LRMV:127-128, threads -> ranks, then -> this rank's groups
+            v.grp = (idx / nranks_) % int(grp_.size());
+        if (v.grp >= 0) {
             SD_CHECK(img && w && kernel, SPIMDECON_ERR_ARG,
                      "img, weight and kernel are required for a view this rank owns (LRMV:401 reads every weight)");
-            DeviceGuard guard(dev_);
+            LrGroup& G = grp_[v.grp];
+            DeviceGuard guard(G.dev);
             v.img.alloc(size_t(n_));
             v.w.alloc(size_t(n_));
-            SD_HIP(hipMemcpyAsync(v.img.p, img, size_t(n_) * 4, hipMemcpyDefault, st_));
-            SD_HIP(hipMemcpyAsync(v.w.p, w, size_t(n_) * 4, hipMemcpyDefault, st_));
-            SD_HIP(hipStreamSynchronize(st_));
+            SD_HIP(hipMemcpyAsync(v.img.p, img, size_t(n_) * 4, hipMemcpyDefault, G.st));
+            SD_HIP(hipMemcpyAsync(v.w.p, w, size_t(n_) * 4, hipMemcpyDefault, G.st));
+            SD_HIP(hipStreamSynchronize(G.st));
             const int64_t kn = int64_t(kd[0]) * kd[1] * kd[2];
             v.kernel.assign(kernel, kernel + kn);
         }
@@ -374,7 +435,6 @@ public:
     double init() {
         SD_CHECK(!inited_, SPIMDECON_ERR_STATE, "lrsim_init called twice");
         SD_CHECK(!views_.empty(), SPIMDECON_ERR_STATE, "no views");
-        DeviceGuard guard(dev_);
         int c[3] = {0, 0, 0};
         int64_t khash = 0;
         for (auto& v : views_)
@@ -393,60 +453,75 @@ public:
         for (int d = 0; d < 3; ++d) pd_.M[d] = fft_fast_size(dims_[d] + 2 * c[d], d == 0);
         g_.Mx = pd_.M[0]; g_.My = pd_.M[1]; g_.Mz = pd_.M[2];
         g_.Sx = pd_.Sx();
-        plan_.create(pd_, st_);
         const size_t R = size_t(pd_.real_floats());
-        psi_.alloc(size_t(n_));
-        Ra_.alloc(R);
-        Rb_.alloc(R);
-        Rc_.alloc(R);
-        value_.alloc(size_t(n_));
-        num_.alloc(size_t(n_));
-        const unsigned gb = grid_of(n_, kB, 4096);
-        part_.alloc(size_t(2) * std::max<unsigned>(gb, grid_of(n_, kB)));
-        red_.alloc(2);
-        // the rank's views (device pointer tables for the per-voxel loops)
-        std::vector<const float*> hp;
-        for (auto& v : views_)
-            if (v.own) hp.push_back(v.img.p);
-        for (auto& v : views_)
-            if (v.own) hp.push_back(v.w.p);
-        nown_ = int(hp.size() / 2);
-        ptrs_.alloc(std::max<size_t>(hp.size(), 1));
-        if (!hp.empty())
-            SD_HIP(hipMemcpyAsync(ptrs_.p, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice, st_));
-        const float* const* d_imgs = reinterpret_cast<const float* const*>(ptrs_.p);
-        const float* const* d_ws = d_imgs + nown_;
-        // kernels: exact-sum normalisation (host), spectra scaled by 1 / (Mx My Mz)
         const float scale = float(1.0 / double(pd_.logical()));
-        DBuf<float> dk;
-        for (auto& v : views_) {
-            if (!v.own) continue;
-            const double s = exact_sum(v.kernel.data(), int64_t(v.kernel.size()));
-            for (auto& t : v.kernel) t = (float)((double)t / s);
-            dk.alloc(v.kernel.size());
-            SD_HIP(hipMemcpyAsync(dk.p, v.kernel.data(), v.kernel.size() * 4, hipMemcpyHostToDevice, st_));
-            v.spec.alloc(R);
-            launch_place_kernel(g_, dk.p, v.kd[0], v.kd[1], v.kd[2], scale, v.spec.p, st_);
-            plan_.forward(v.spec.p);
-            SD_HIP(hipStreamSynchronize(st_));
+        const unsigned gb = grid_of(n_, kB, 4096);
+        for (size_t gi = 0; gi < grp_.size(); ++gi) {
+            LrGroup& G = grp_[gi];
+            DeviceGuard guard(G.dev);
+            G.plan.create(pd_, G.st);
+            G.psi.alloc(size_t(n_));
+            G.Ra.alloc(R);
+            G.Rb.alloc(R);
+            G.Rc.alloc(R);
+            G.value.alloc(size_t(n_));
+            G.num.alloc(size_t(n_));
+            if (gi == 0 && grp_.size() > 1) G.tmp.alloc(size_t(n_));
+            std::vector<const float*> hp;
+            for (auto& v : views_)
+                if (v.grp == int(gi)) hp.push_back(v.img.p);
+            for (auto& v : views_)
+                if (v.grp == int(gi)) hp.push_back(v.w.p);
+            G.nown = int(hp.size() / 2);
+            G.ptrs.alloc(std::max<size_t>(hp.size(), 1));
+            if (!hp.empty())
+                SD_HIP(hipMemcpyAsync(G.ptrs.p, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice, G.st));
+            // kernels: exact-sum normalisation (host), spectra scaled by 1 / (Mx My Mz)
+            DBuf<float> dk;
+            for (auto& v : views_) {
+                if (v.grp != int(gi)) continue;
+                const double s = exact_sum(v.kernel.data(), int64_t(v.kernel.size()));
+                for (auto& t : v.kernel) t = (float)((double)t / s);
+                dk.alloc(v.kernel.size());
+                SD_HIP(hipMemcpyAsync(dk.p, v.kernel.data(), v.kernel.size() * 4, hipMemcpyHostToDevice, G.st));
+                v.spec.alloc(R);
+                launch_place_kernel(g_, dk.p, v.kd[0], v.kd[1], v.kd[2], scale, v.spec.p, G.st);
+                G.plan.forward(v.spec.p);
+                SD_HIP(hipStreamSynchronize(G.st));
+            }
+            // normAllImages: the group's per-voxel partials {sum of img where w != 0, count}
+            hipLaunchKernelGGL(k_lr_overlap, dim3(gb), dim3(kB), 0, G.st, n_, G.nown, imgs_of(G), ws_of(G),
+                               G.value.p, G.num.p);
+            SD_HIP(hipGetLastError());
         }
-        // normAllImages: per-voxel partials of the rank, summed over ranks
-        hipLaunchKernelGGL(k_lr_overlap, dim3(gb), dim3(kB), 0, st_, n_, nown_, d_imgs, d_ws, value_.p, num_.p);
-        SD_HIP(hipGetLastError());
-        allreduce(value_.p, n_, ncclSum);
-        allreduce(num_.p, n_, ncclSum);
-        hipLaunchKernelGGL(k_lr_avg_partials, dim3(gb), dim3(kB), 0, st_, n_, value_.p, num_.p, part_.p);
-        hipLaunchKernelGGL(k_lr_sum2, dim3(1), dim3(1024), 0, st_, part_.p, int64_t(gb), red_.p);
+        LrGroup& G0 = grp_[0];
+        DeviceGuard guard(G0.dev);
+        part_.alloc(size_t(2) * gb);
+        red_.alloc(2);
+        merge_groups(&LrGroup::value, false);
+        merge_groups(&LrGroup::num, false);
+        allreduce(G0.value.p, n_, ncclSum);
+        allreduce(G0.num.p, n_, ncclSum);
+        hipLaunchKernelGGL(k_lr_avg_partials, dim3(gb), dim3(kB), 0, G0.st, n_, G0.value.p, G0.num.p, part_.p);
+        hipLaunchKernelGGL(k_lr_sum2, dim3(1), dim3(1024), 0, G0.st, part_.p, int64_t(gb), red_.p);
         SD_HIP(hipGetLastError());
         double r[2];
-        SD_HIP(hipMemcpyAsync(r, red_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
+        SD_HIP(hipMemcpyAsync(r, red_.p, sizeof(r), hipMemcpyDeviceToHost, G0.st));
         wait();
         avg_ = r[1] == 0.0 ? 1.0 : r[0] / r[1];
-        launch_fill(psi_.p, n_, (float)avg_, st_);
-        // num = sum of the weights > 0 (constant over the iterations): reduced once
-        hipLaunchKernelGGL(k_lr_num, dim3(gb), dim3(kB), 0, st_, n_, nown_, d_ws, num_.p);
-        SD_HIP(hipGetLastError());
-        allreduce(num_.p, n_, ncclSum);
+        // num = sum of the weights > 0 (constant over the iterations): merged and reduced once
+        for (auto& G : grp_) {
+            DeviceGuard g2(G.dev);
+            launch_fill(G.psi.p, n_, (float)avg_, G.st);
+            hipLaunchKernelGGL(k_lr_num, dim3(gb), dim3(kB), 0, G.st, n_, G.nown, ws_of(G), G.num.p);
+            SD_HIP(hipGetLastError());
+        }
+        merge_groups(&LrGroup::num, false);
+        allreduce(G0.num.p, n_, ncclSum);
+        for (auto& G : grp_) {
+            DeviceGuard g2(G.dev);
+            SD_HIP(hipStreamSynchronize(G.st));
+        }
         wait();
         inited_ = true;
         return avg_;
@@ -456,8 +531,8 @@ public:
         SD_CHECK(inited_, SPIMDECON_ERR_STATE, "lrsim_init first");
         SD_CHECK(!dead_, SPIMDECON_ERR_STATE, "communicator aborted");
         SD_CHECK(iters >= 0, SPIMDECON_ERR_ARG, "iters must be >= 0");
-        DeviceGuard guard(dev_);
         {
+            DeviceGuard guard(grp_[0].dev);
             int64_t lb;
             std::memcpy(&lb, &lambda, 8);
             const int64_t mine[4] = {0x4c52534d32LL, iters, int64_t(mult), lb};
@@ -467,35 +542,44 @@ public:
         const unsigned gr = grid_of(g_.My * g_.Mz, kW);
         const unsigned gi = grid_of(g_.ny * g_.nz, kW);
         const unsigned gb = grid_of(n_, kB);
+        LrGroup& G0 = grp_[0];
         for (int it = 0; it < iters; ++it) {
-            launch_pad_mirror(g_, psi_.p, Ra_.p, st_);
-            plan_.forward(Ra_.p);
-            hipLaunchKernelGGL(k_lr_fill, dim3(grid_of(n_, kB, 4096)), dim3(kB), 0, st_, value_.p, n_,
-                               mult ? 1.0 : 0.0);
-            for (auto& v : views_) {
-                if (!v.own) continue;
-                hipLaunchKernelGGL(k_lr_cmul, dim3(grid_of(ncplx / 2, kB, 256 * 32)), dim3(kB), 0, st_,
-                                   reinterpret_cast<const float4*>(Ra_.p), reinterpret_cast<const float4*>(v.spec.p),
-                                   reinterpret_cast<float4*>(Rb_.p), ncplx / 2,
-                                   reinterpret_cast<const float2*>(Ra_.p) + (ncplx - 1),
-                                   reinterpret_cast<const float2*>(v.spec.p) + (ncplx - 1),
-                                   reinterpret_cast<float2*>(Rb_.p) + (ncplx - 1), int(ncplx & 1));
-                plan_.inverse(Rb_.p);   // blurred = conv(psi, K) at the interior slots
-                hipLaunchKernelGGL(k_lr_quot_pad, dim3(gr), dim3(kB), 0, st_, g_, v.img.p, Rb_.p, Rc_.p);
-                plan_.forward(Rc_.p);
-                launch_spec_mul(Rc_.p, v.spec.p, ncplx, st_);
-                plan_.inverse(Rc_.p);   // the view's contribution conv(img / blurred, K)
-                if (mult)
-                    hipLaunchKernelGGL(k_lr_accum<true>, dim3(gi), dim3(kB), 0, st_, g_, Rc_.p, v.w.p, value_.p);
-                else
-                    hipLaunchKernelGGL(k_lr_accum<false>, dim3(gi), dim3(kB), 0, st_, g_, Rc_.p, v.w.p, value_.p);
-                SD_HIP(hipGetLastError());
+            for (auto& G : grp_) {   // every group's views, concurrently on their own streams
+                DeviceGuard guard(G.dev);
+                launch_pad_mirror(g_, G.psi.p, G.Ra.p, G.st);
+                G.plan.forward(G.Ra.p);
+                hipLaunchKernelGGL(k_lr_fill, dim3(grid_of(n_, kB, 4096)), dim3(kB), 0, G.st, G.value.p, n_,
+                                   mult ? 1.0 : 0.0);
+                for (auto& v : views_) {
+                    if (v.grp != int(&G - grp_.data())) continue;
+                    hipLaunchKernelGGL(k_lr_cmul, dim3(grid_of(ncplx / 2, kB, 256 * 32)), dim3(kB), 0, G.st,
+                                       reinterpret_cast<const float4*>(G.Ra.p),
+                                       reinterpret_cast<const float4*>(v.spec.p), reinterpret_cast<float4*>(G.Rb.p),
+                                       ncplx / 2, reinterpret_cast<const float2*>(G.Ra.p) + (ncplx - 1),
+                                       reinterpret_cast<const float2*>(v.spec.p) + (ncplx - 1),
+                                       reinterpret_cast<float2*>(G.Rb.p) + (ncplx - 1), int(ncplx & 1));
+                    G.plan.inverse(G.Rb.p);   // blurred = conv(psi, K) at the interior slots
+                    hipLaunchKernelGGL(k_lr_quot_pad, dim3(gr), dim3(kB), 0, G.st, g_, v.img.p, G.Rb.p, G.Rc.p);
+                    G.plan.forward(G.Rc.p);
+                    launch_spec_mul(G.Rc.p, v.spec.p, ncplx, G.st);
+                    G.plan.inverse(G.Rc.p);   // the view's contribution conv(img / blurred, K)
+                    if (mult)
+                        hipLaunchKernelGGL(k_lr_accum<true>, dim3(gi), dim3(kB), 0, G.st, g_, G.Rc.p, v.w.p,
+                                           G.value.p);
+                    else
+                        hipLaunchKernelGGL(k_lr_accum<false>, dim3(gi), dim3(kB), 0, G.st, g_, G.Rc.p, v.w.p,
+                                           G.value.p);
+                    SD_HIP(hipGetLastError());
+                }
             }
-            // the compound correction of all views: one all-reduce (product / sum over ranks)
-            allreduce(value_.p, n_, mult ? ncclProd : ncclSum);
+            DeviceGuard guard(G0.dev);
+            // the compound correction of all views: merged over the groups, then one all-reduce
+            // (product / sum) over the ranks
+            merge_groups(&LrGroup::value, mult);
+            allreduce(G0.value.p, n_, mult ? ncclProd : ncclSum);
             auto upd = [&](auto m, auto t) {
-                hipLaunchKernelGGL((k_lr_update<decltype(m)::value, decltype(t)::value>), dim3(gb), dim3(kB), 0, st_,
-                                   n_, psi_.p, value_.p, num_.p, lambda, part_.p);
+                hipLaunchKernelGGL((k_lr_update<decltype(m)::value, decltype(t)::value>), dim3(gb), dim3(kB), 0,
+                                   G0.st, n_, G0.psi.p, G0.value.p, G0.num.p, lambda, part_.p);
             };
             using T = std::true_type;
             using F = std::false_type;
@@ -504,9 +588,19 @@ public:
             else if (lambda > 0) upd(F{}, T{});
             else upd(F{}, F{});
             SD_HIP(hipGetLastError());
-            launch_reduce_partials(part_.p, int64_t(gb), red_.p, 0, st_);
+            launch_reduce_partials(part_.p, int64_t(gb), red_.p, 0, G0.st);
+            // the new psi to the other groups (on group 0's stream; they wait for it)
+            for (size_t g = 1; g < grp_.size(); ++g)
+                SD_HIP(hipMemcpyAsync(grp_[g].psi.p, G0.psi.p, size_t(n_) * 4, hipMemcpyDefault, G0.st));
+            if (grp_.size() > 1) {
+                SD_HIP(hipEventRecord(G0.ev, G0.st));
+                for (size_t g = 1; g < grp_.size(); ++g) {
+                    DeviceGuard g2(grp_[g].dev);
+                    SD_HIP(hipStreamWaitEvent(grp_[g].st, G0.ev, 0));
+                }
+            }
             double r[2];
-            SD_HIP(hipMemcpyAsync(r, red_.p, sizeof(r), hipMemcpyDeviceToHost, st_));
+            SD_HIP(hipMemcpyAsync(r, red_.p, sizeof(r), hipMemcpyDeviceToHost, G0.st));
             wait();
             if (stats) {
                 stats[2 * it] = r[0];
@@ -518,14 +612,19 @@ public:
     void get_psi(float* out) {
         SD_CHECK(inited_, SPIMDECON_ERR_STATE, "lrsim_init first");
         SD_CHECK(out, SPIMDECON_ERR_ARG, "null argument");
-        DeviceGuard guard(dev_);
-        SD_HIP(hipMemcpyAsync(out, psi_.p, size_t(n_) * 4, hipMemcpyDefault, st_));
+        DeviceGuard guard(grp_[0].dev);
+        SD_HIP(hipMemcpyAsync(out, grp_[0].psi.p, size_t(n_) * 4, hipMemcpyDefault, grp_[0].st));
         wait();
     }
 
     int owns(int v) const {
         SD_CHECK(v >= 0 && v < int(views_.size()), SPIMDECON_ERR_ARG, "bad view index");
-        return views_[v].own ? 1 : 0;
+        return views_[v].grp >= 0 ? 1 : 0;
+    }
+
+    int view_device(int v) const {
+        SD_CHECK(v >= 0 && v < int(views_.size()), SPIMDECON_ERR_ARG, "bad view index");
+        return views_[v].grp >= 0 ? grp_[views_[v].grp].dev : -1;
     }
 
     void fft_dims(int64_t* out3) const {
@@ -534,23 +633,47 @@ public:
     }
 
 private:
-    void allreduce(double* p, int64_t n, ncclRedOp_t op) {
-        if (!comm_) return;
-        SD_NCCL_LR(ncclAllReduce(p, p, size_t(n), ncclDouble, op, comm_, st_));
+    static const float* const* imgs_of(const LrGroup& G) { return reinterpret_cast<const float* const*>(G.ptrs.p); }
+    static const float* const* ws_of(const LrGroup& G) { return imgs_of(G) + G.nown; }
+
+    // group 0's array (member `a`) merged with every other group's, in group order, on group
+    // 0's stream after their streams' work so far: a sum, or a product (mult)
+    void merge_groups(DBuf<double> LrGroup::*a, bool mult) {
+        if (grp_.size() < 2) return;
+        LrGroup& G0 = grp_[0];
+        for (size_t g = 1; g < grp_.size(); ++g) {
+            LrGroup& G = grp_[g];
+            {
+                DeviceGuard guard(G.dev);
+                SD_HIP(hipEventRecord(G.ev, G.st));
+            }
+            DeviceGuard guard(G0.dev);
+            SD_HIP(hipStreamWaitEvent(G0.st, G.ev, 0));
+            SD_HIP(hipMemcpyAsync(G0.tmp.p, (G.*a).p, size_t(n_) * 8, hipMemcpyDefault, G0.st));
+            hipLaunchKernelGGL(k_lr_merge, dim3(grid_of(n_, kB, 4096)), dim3(kB), 0, G0.st, (G0.*a).p, G0.tmp.p, n_,
+                               int(mult));
+            SD_HIP(hipGetLastError());
+        }
     }
 
-    // waits for the stream; with a communicator, bounded: an asynchronous RCCL error or
+    void allreduce(double* p, int64_t n, ncclRedOp_t op) {
+        if (!comm_) return;
+        SD_NCCL_LR(ncclAllReduce(p, p, size_t(n), ncclDouble, op, comm_, grp_[0].st));
+    }
+
+    // waits for group 0's stream; with a communicator, bounded: an asynchronous RCCL error or
     // SPIMDECON_RCCL_TIMEOUT seconds without completion abort it (ranks that disagree on
     // the work fail instead of waiting for each other forever)
     void wait() {
+        hipStream_t st = grp_[0].st;
         if (!comm_) {
-            SD_HIP(hipStreamSynchronize(st_));
+            SD_HIP(hipStreamSynchronize(st));
             return;
         }
         const auto t0 = std::chrono::steady_clock::now();
         int spins = 0;
         for (;;) {
-            const hipError_t e = hipStreamQuery(st_);
+            const hipError_t e = hipStreamQuery(st);
             if (e == hipSuccess) return;
             if (e != hipErrorNotReady) SD_HIP(e);
             ncclResult_t ar = ncclSuccess;
@@ -571,14 +694,16 @@ private:
     }
 
     // every rank's K values all-gathered; refused on every rank unless all are equal
-    // (index 1.. hold what must match; a mismatch would post different collectives)
+    // (a mismatch would post different collectives)
     void agree(const int64_t* mine, int K, const char* what) {
         if (!comm_) return;
+        hipStream_t st = grp_[0].st;
+        DeviceGuard guard(grp_[0].dev);
         DBuf<int64_t> d(size_t(K) * nranks_);
         std::vector<int64_t> all(size_t(K) * nranks_);
-        SD_HIP(hipMemcpyAsync(d.p + size_t(K) * rank_, mine, size_t(K) * 8, hipMemcpyHostToDevice, st_));
-        SD_NCCL_LR(ncclAllGather(d.p + size_t(K) * rank_, d.p, size_t(K), ncclInt64, comm_, st_));
-        SD_HIP(hipMemcpyAsync(all.data(), d.p, all.size() * 8, hipMemcpyDeviceToHost, st_));
+        SD_HIP(hipMemcpyAsync(d.p + size_t(K) * rank_, mine, size_t(K) * 8, hipMemcpyHostToDevice, st));
+        SD_NCCL_LR(ncclAllGather(d.p + size_t(K) * rank_, d.p, size_t(K), ncclInt64, comm_, st));
+        SD_HIP(hipMemcpyAsync(all.data(), d.p, all.size() * 8, hipMemcpyDeviceToHost, st));
         wait();
         for (int r = 0; r < nranks_; ++r)
             for (int k = 0; k < K; ++k)
@@ -590,21 +715,17 @@ private:
 
     int64_t dims_[3] = {0, 0, 0};
     int64_t n_ = 0;
-    int dev_ = 0, nranks_ = 1, rank_ = 0, nown_ = 0;
-    hipStream_t st_ = nullptr;
+    int nranks_ = 1, rank_ = 0;
     ncclComm_t comm_ = nullptr;
     double timeout_s_ = 300.0;
     bool dead_ = false, inited_ = false;
     double avg_ = 1.0;
     std::vector<LrView> views_;
+    std::vector<LrGroup> grp_;
     SlabGeom g_{};
     PadDims pd_;
-    FftPlan3D plan_;
-    DBuf<float> psi_, Ra_, Rb_, Rc_;
-    DBuf<double> value_, num_, part_, red_;
-    DBuf<const float*> ptrs_;
+    DBuf<double> part_, red_;   // (group 0)
 };
-
 }  // namespace spimdecon
 
 using spimdecon::guarded;
@@ -624,8 +745,25 @@ int lrsim_create(const int64_t* dims, int device, int nranks, int rank, const ch
     return guarded([&] {
         SD_CHECK(out, SPIMDECON_ERR_ARG, "null argument");
         *out = nullptr;
-        auto s = std::make_unique<LrSim>(dims, device, nranks, rank, comm_id);
+        auto s = std::make_unique<LrSim>(dims, std::vector<int>{device}, nranks, rank, comm_id);
         *out = new lrsim_session{s.release()};
+    });
+}
+
+int lrsim_create_devices(const int64_t* dims, const int* devs, int ndev, lrsim_session** out) {
+    return guarded([&] {
+        SD_CHECK(out && devs && ndev >= 1, SPIMDECON_ERR_ARG, "null argument");
+        *out = nullptr;
+        auto s = std::make_unique<LrSim>(dims, std::vector<int>(devs, devs + ndev), 1, 0, nullptr);
+        *out = new lrsim_session{s.release()};
+    });
+}
+
+int lrsim_view_device(lrsim_session* h, int view, int* device) {
+    return guarded([&] {
+        LRS(h);
+        SD_CHECK(device, SPIMDECON_ERR_ARG, "null argument");
+        *device = S.view_device(view);
     });
 }
 

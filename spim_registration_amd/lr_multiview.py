@@ -78,11 +78,14 @@ class LucyRichardsonMultiViewDeconvolution:
 
 def lucy_richardson_multi_view(data, max_iterations: int, multiplicative: bool, lambda_: float, device: int = 0,
                                nranks: int = 1, rank: int = 0, comm_id: bytes | None = None,
-                               stats_out: list | None = None, avg_out: list | None = None) -> np.ndarray:
+                               stats_out: list | None = None, avg_out: list | None = None,
+                               devices=None) -> np.ndarray:
     """Runs LucyRichardsonMultiViewDeconvolution.lucyRichardsonMultiView (:24-358) and
     returns psi.  ``minIterations`` of the reference is unused there too; the do-while
     (:98-351) runs max(1, maxIterations) iterations.  ``stats_out`` receives
-    (sumChange, maxChange) per iteration, ``avg_out`` the initial average (:63)."""
+    (sumChange, maxChange) per iteration, ``avg_out`` the initial average (:63).
+    ``devices``: several GPUs of this process (view v on devices[v % len]; ids may
+    repeat), as the reference's threads; not combined with RCCL ranks."""
     if not data:
         raise ValueError("no views")
     lib = _lib.load()
@@ -97,7 +100,13 @@ def lucy_richardson_multi_view(data, max_iterations: int, multiplicative: bool, 
     d = (C.c_int64 * 3)(nx, ny, nz)
     h = C.c_void_p()
     cid = None if comm_id is None else C.create_string_buffer(bytes(comm_id), 128)
-    check(lib.lrsim_create(d, int(device), int(nranks), int(rank), cid, C.byref(h)))
+    if devices is not None:
+        if nranks != 1 or comm_id is not None:
+            raise ValueError("devices and RCCL ranks cannot be combined")
+        dv = (C.c_int * len(devices))(*[int(x) for x in devices])
+        check(lib.lrsim_create_devices(d, dv, len(devices), C.byref(h)))
+    else:
+        check(lib.lrsim_create(d, int(device), int(nranks), int(rank), cid, C.byref(h)))
     try:
         for i, v in enumerate(data):
             kz, ky, kx = v.kernel.shape

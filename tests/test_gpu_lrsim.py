@@ -93,3 +93,37 @@ def test_lrsim_errors(gpu):
         assert lib.lrsim_init(h, None) != 0                             # no views
     finally:
         lib.lrsim_destroy(h)
+
+
+@pytest.mark.parametrize("mult", [False, True])
+def test_lrsim_device_groups_merge(gpu, mult):
+    # three groups on one GPU (repeated ids: the multi-GPU code path -- per-group streams and
+    # plans, the partials merged on group 0, psi copied back): view v on group v % 3 of 4
+    # views, against one group and against the oracle's merge of the same per-group partials
+    imgs, ws, psfs = _views(n=4, shape=(28, 24, 30))
+    data = [LucyRichardsonFFT(i, w, k) for i, w, k in zip(imgs, ws, psfs)]
+    s1, s3 = [], []
+    one = lucy_richardson_multi_view(data, 2, mult, 0.006, device=gpu, stats_out=s1)
+    three = lucy_richardson_multi_view(data, 2, mult, 0.006, devices=[gpu] * 3, stats_out=s3)
+    assert rel_l2(three, one) < 1e-6
+    np.testing.assert_allclose(np.array(s3), np.array(s1), rtol=1e-6)
+    exp, _, _ = ref.lucy_richardson_multi_view(imgs, ws, psfs, 2, mult, 0.006, views_of=[[0, 3], [1], [2]])
+    assert rel_l2(three, exp) < TOL
+    lib = _lib.load()
+    import ctypes as C
+    d = (C.c_int64 * 3)(8, 8, 8)
+    dv = (C.c_int * 2)(gpu, gpu)
+    h = C.c_void_p()
+    _lib.check(lib.lrsim_create_devices(d, dv, 2, C.byref(h)))
+    try:
+        kd = np.array([3, 3, 3], np.int32)
+        k = np.ones((3, 3, 3), np.float32)
+        z = np.ones((8, 8, 8), np.float32)
+        for _ in range(3):
+            _lib.check(lib.lrsim_add_view(h, z.ctypes.data, z.ctypes.data, k.ctypes.data, kd.ctypes.data_as(_lib._pi)))
+        dev = C.c_int()
+        for v in range(3):
+            _lib.check(lib.lrsim_view_device(h, v, C.byref(dev)))
+            assert dev.value == gpu
+    finally:
+        lib.lrsim_destroy(h)
