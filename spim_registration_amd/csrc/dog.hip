@@ -441,7 +441,7 @@ __device__ __forceinline__ DzBox xcd_box(bool xcd) {
 // a second item, and the blocks of a CU run their phases in step, so the SIMDs of those
 // waves set the pace: no gain at 48), 4 blocks per CU; 768^3: k_dog_xy 1.63 -> 1.47 ms,
 // DoG 3.67 -> 3.52 ms (profiles/r05_dog_strips_ab.txt).
-template <int KW, int TY, bool BUF = true>
+template <int KW, int TY, bool BUF = true, int JT = 0>
 __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
                                                 const float* __restrict__ mm, int xcd, int mm_exact) {
@@ -476,6 +476,14 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
     // a = 0 is +0: every a is in the reciprocal path's exact range (NaN stays NaN either
     // way), so the per-value range check is skipped for the whole launch
     const bool allfast = norm && mm_exact != 0 && rd != 0.0f && fabsf(mn) >= 0x1p-20f;
+    // Tap trim: the JT leading (and trailing) taps of the x and y kernels are zero for both
+    // sigmas (padded to KW; the host instantiates JT).  When k_minmax found every value
+    // finite (mm[2] == 0) and the image is normalised by its own range, every staged value
+    // lies in [0, 1] and every partial sum is finite and never -0 (it starts at +0; the
+    // taps are >= 0), so such a tap's +-0 product leaves the sum's bits unchanged: skipped.
+    // Otherwise (NaN / inf in the image, a caller-given range) every padded tap is applied,
+    // as before (one uniform branch per item between the two unrolled tap loops).
+    const bool trim = JT > 0 && mm && norm && mm_exact != 0 && mm[2] == 0.0f;
     // thread t stages column t % IPC (IPC = IP rounded up so three rows fit 256 threads)
     // of rows t / IPC, t / IPC + RPT, ...: the column's mirror index once, the row's per
     // load.  Steps whose staged box lies inside the volume index without the mirror
@@ -574,12 +582,17 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
             dg_v2 acc[kDxySeg];
 #pragma unroll
             for (int o = 0; o < kDxySeg; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+            auto taps = [&](auto j0c) {
+                constexpr int J0 = decltype(j0c)::value;
 #pragma unroll
-            for (int j = 0; j < KW; ++j) {
-                const dg_v2 k = dg_v2{kx[j].x, kx[j].y};
+                for (int j = J0; j < KW - J0; ++j) {
+                    const dg_v2 k = dg_v2{kx[j].x, kx[j].y};
 #pragma unroll
-                for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
-            }
+                    for (int o = 0; o < kDxySeg; ++o) acc[o] = acc[o] + dg_v2{w[o + j], w[o + j]} * k;  // tap order kept
+                }
+            };
+            if (trim) taps(std::integral_constant<int, JT>{});
+            else taps(std::integral_constant<int, 0>{});
             float2* dst = sx + (xrow0 + row) * kDxySxP + seg * kDxySeg;
 #pragma unroll
             for (int o = 0; o < kDxySeg; ++o) dst[o] = make_float2(acc[o].x, acc[o].y);
@@ -642,12 +655,17 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
             dg_v2 acc[OY];
 #pragma unroll
             for (int o = 0; o < OY; ++o) acc[o] = dg_v2{0.0f, 0.0f};
+            auto taps = [&](auto j0c) {
+                constexpr int J0 = decltype(j0c)::value;
 #pragma unroll
-            for (int j = 0; j < KW; ++j) {
-                const dg_v2 k = dg_v2{ky[j].x, ky[j].y};
+                for (int j = J0; j < KW - J0; ++j) {
+                    const dg_v2 k = dg_v2{ky[j].x, ky[j].y};
 #pragma unroll
-                for (int o = 0; o < OY; ++o) acc[o] = acc[o] + w[o + j] * k;
-            }
+                    for (int o = 0; o < OY; ++o) acc[o] = acc[o] + w[o + j] * k;
+                }
+            };
+            if (trim) taps(std::integral_constant<int, JT>{});
+            else taps(std::integral_constant<int, 0>{});
 #pragma unroll
             for (int o = 0; o < OY; ++o) {
                 const int y = y0 + run * OY + o;
@@ -1227,7 +1245,9 @@ __global__ __launch_bounds__(256) void k_dog_peaks(Dims3 d, const float* __restr
 __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in, int64_t n,
                                                     float* __restrict__ partial) {
     __shared__ float smn[kBlock / 64], smx[kBlock / 64];
+    __shared__ int sbad[kBlock / 64];
     float mn = INFINITY, mx = -INFINITY;
+    float z = 0.0f;   // v * 0 summed: NaN once any value is NaN or infinite (finite: +-0)
     const int64_t stride = int64_t(gridDim.x) * kBlock;
     const int64_t t0 = int64_t(blockIdx.x) * kBlock + threadIdx.x;
     if ((reinterpret_cast<uintptr_t>(in) & 15u) == 0) {   // 16-B loads, then the tail
@@ -1237,52 +1257,64 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float* __restrict__ in,
             const float4 v = in4[i];
             mn = fminf(fminf(mn, v.x), fminf(v.y, fminf(v.z, v.w)));
             mx = fmaxf(fmaxf(mx, v.x), fmaxf(v.y, fmaxf(v.z, v.w)));
+            z += (v.x * 0.0f + v.y * 0.0f) + (v.z * 0.0f + v.w * 0.0f);
         }
         for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
             mn = fminf(mn, in[i]);
             mx = fmaxf(mx, in[i]);
+            z += in[i] * 0.0f;
         }
     } else {
         for (int64_t i = t0; i < n; i += stride) {
             const float v = in[i];
             mn = fminf(mn, v);
             mx = fmaxf(mx, v);
+            z += v * 0.0f;
         }
     }
+    int bad = isnan(z) ? 1 : 0;
     for (int off = 32; off > 0; off >>= 1) {
         mn = fminf(mn, __shfl_xor(mn, off, 64));
         mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        bad |= __shfl_xor(bad, off, 64);
     }
     if ((threadIdx.x & 63) == 0) {
         smn[threadIdx.x >> 6] = mn;
         smx[threadIdx.x >> 6] = mx;
+        sbad[threadIdx.x >> 6] = bad;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kBlock / 64; ++w) {
             mn = fminf(mn, smn[w]);
             mx = fmaxf(mx, smx[w]);
+            bad |= sbad[w];
         }
         partial[2 * blockIdx.x] = mn;
         partial[2 * blockIdx.x + 1] = mx;
+        partial[2 * gridDim.x + blockIdx.x] = bad ? 1.0f : 0.0f;
     }
 }
 
 // min / max over the per-block partials: one wave, lane-strided then shuffles
 // (min and max are order-independent, so the result equals a sequential scan)
+// partial[2] = 1 when any value is NaN or infinite, else 0 (k_dog_xy's tap trim)
 __global__ __launch_bounds__(64) void k_minmax_final(float* partial, int nb) {
-    float mn = INFINITY, mx = -INFINITY;
+    float mn = INFINITY, mx = -INFINITY, bad = 0.0f;
     for (int b = threadIdx.x; b < nb; b += 64) {
         mn = fminf(mn, partial[2 * b]);
         mx = fmaxf(mx, partial[2 * b + 1]);
+        bad = fmaxf(bad, partial[2 * nb + b]);
     }
     for (int off = 32; off > 0; off >>= 1) {
         mn = fminf(mn, __shfl_xor(mn, off, 64));
         mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        bad = fmaxf(bad, __shfl_xor(bad, off, 64));
     }
     if (threadIdx.x == 0) {
         partial[0] = mn;
         partial[1] = mx;
+        partial[2] = bad;
     }
 }
 
@@ -1722,6 +1754,17 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     SD_HIP(hipMemcpyAsync(w.taps.p, kall.data(), kall.size() * 4, hipMemcpyHostToDevice, s));
     auto kp = [&](int axis, int which) { return w.taps.p + (2 * axis + which) * K; };
     auto kp2 = [&](int axis) { return reinterpret_cast<const float2*>(w.taps.p + 6 * K + 2 * axis * K); };
+    // leading taps zero for both sigmas along an axis (k_dog_xy may skip them, see there)
+    auto zero_lead = [&](int a) {
+        int t = 0;
+        while (t < K / 2 && k1[a][t] == 0.0f && k2[a][t] == 0.0f && k1[a][K - 1 - t] == 0.0f &&
+               k2[a][K - 1 - t] == 0.0f)
+            ++t;
+        return t;
+    };
+    // (instantiated for 0 and 1 trimmed taps -- 1 at the default sigma 1.8; 2 spilled VGPRs)
+    // (SPIMDECON_DOG_TRIM=0: every padded tap always)
+    const int jt = dog_env("SPIMDECON_DOG_TRIM", 1) ? std::min(1, std::min(zero_lead(0), zero_lead(1))) : 0;
 
     // the view: read in place when it already lives in HBM, else one upload
     const float* in = img;
@@ -1730,13 +1773,14 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         SD_HIP(hipMemcpyAsync(w.in.p, img, n * 4, hipMemcpyDefault, s));   // host or another device
         in = w.in.p;
     }
-    grow(w.mm, 2 * 4096);
+    grow(w.mm, 3 * 4096);
     const bool use_given = !(std::isnan(p->min_intensity) || std::isnan(p->max_intensity) ||
                              std::isinf(p->min_intensity) || std::isinf(p->max_intensity) ||
                              p->min_intensity == p->max_intensity);
     if (use_given) {
-        const float h2[2] = {float(p->min_intensity), float(p->max_intensity)};
-        SD_HIP(hipMemcpyAsync(w.mm.p, h2, 8, hipMemcpyHostToDevice, s));
+        // (mm[2] = 1: values not scanned, k_dog_xy keeps every padded tap)
+        const float h2[3] = {float(p->min_intensity), float(p->max_intensity), 1.0f};
+        SD_HIP(hipMemcpyAsync(w.mm.p, h2, 12, hipMemcpyHostToDevice, s));
     } else {
         const unsigned nb = grid_of(n);
         hipLaunchKernelGGL(k_minmax, dim3(nb), dim3(kBlock), 0, s, in, n, w.mm.p);
@@ -1795,11 +1839,13 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         // (k_minmax's own range: the per-value range check is skipped; SPIMDECON_DOG_MM_EXACT=0
         // keeps it -- 1.52-1.62 vs 1.66 ms per 768^3, bit-exact, gpu_r3z11.sh)
         const int mmx = !use_given && dog_env("SPIMDECON_DOG_MM_EXACT", 1) != 0 ? 1 : 0;
-#define SD_DOGXY(KV)                                                                                        \
-        if (xbuf) hipLaunchKernelGGL((k_dog_xy<KV, ty, true>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
-        else hipLaunchKernelGGL((k_dog_xy<KV, ty, false>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
+#define SD_DOGXY3(KV, JV)                                                                                   \
+        if (xbuf) hipLaunchKernelGGL((k_dog_xy<KV, ty, true, JV>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, ty, false, JV>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
+#define SD_DOGXY(KV) if (jt == 1) { SD_DOGXY3(KV, 1) } else { SD_DOGXY3(KV, 0) }
         if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
+#undef SD_DOGXY3
         SD_HIP(hipGetLastError());
         if (split) {
             const int64_t waves = ceil_div(d.nx, int64_t(64)) * d.ny;

@@ -265,3 +265,26 @@ def test_dog_own_range_division_edges(gpu, monkeypatch):
     exp, dref = dog_ref.process_dog(img, 1.8, 1e-9, find_min=True, find_max=True)
     np.testing.assert_array_equal(out["1"][1], dref)
     assert [tuple(int(c) for c in q[0]) for q in out["1"][0]] == [e[:3] for e in exp]
+
+
+@pytest.mark.parametrize("sigma", [1.0, 1.8, 4.0])
+def test_dog_zero_tap_trim_bit_identical(gpu, sigma, monkeypatch):
+    """k_dog_xy skips the padded taps that are zero for both sigmas when k_minmax found
+    every value finite and normalised the image by its own range (SPIMDECON_DOG_TRIM=1,
+    the default): the DoG image and the ordered peaks equal those of every padded tap (=0)
+    bit for bit.  With a NaN or an infinity in the image the trim is off, so the NaN
+    footprint stays that of all padded taps."""
+    img = bead_stack(shape=(40, 44, 48), cid=27)
+    nan_img = img.copy()
+    nan_img[20, 22, 24] = np.nan
+    inf_img = img.copy()
+    inf_img[7, 30, 11] = np.inf
+    for im in (img, nan_img, inf_img):
+        out = {}
+        for t in ("1", "0"):
+            monkeypatch.setenv("SPIMDECON_DOG_TRIM", t)
+            pk, d = dog.compute(im, sigma=sigma, threshold=1e-4, find_min=True, find_max=True, return_dog=True,
+                                keep_intensity=True)
+            out[t] = ([(tuple(p.location), p.intensity) for p in pk], d)
+        np.testing.assert_array_equal(out["1"][1], out["0"][1])
+        assert out["1"][0] == out["0"][0]
