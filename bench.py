@@ -90,7 +90,15 @@ def parse(argv=None):
     ap.add_argument("--c5-rank", action="store_true",
                     help="BASELINE configs[4] per rank: the 2048x256x1024 y-slab one of 8 ranks holds "
                          "(padded 2100x1050x280 internally), fp16 img/weight storage, OPTIMIZATION_I 0.006")
+    ap.add_argument("--c3-rank", action="store_true",
+                    help="BASELINE configs[2] per rank: the 1024x128x512 y-slab one of 8 ranks holds "
+                         "(padded 1050x540x152 internally), EFFICIENT_BAYESIAN 0.006")
     a = ap.parse_args(argv)
+    if a.c3_rank:
+        a.shape = [1024, 128, 512]
+        a.slab_axis = "y"
+        a.psftype, a.lam = "EFFICIENT_BAYESIAN", 0.006
+        a.no_strong_line = a.no_default_mode = True
     if a.c5_rank:
         a.shape = [2048, 256, 1024]
         a.fp16, a.slab_axis = True, "y"
@@ -555,6 +563,8 @@ def main(argv=None):
                                      + f" per GPU (global {nx}x{ny_g}x{nz_g})")
                                     + (" (one rank's y-slab of BASELINE configs[4], 2048x2048x1024 over 8 ranks)"
                                        if args.c5_rank else "")
+                                    + (" (one rank's y-slab of BASELINE configs[2], 1024x1024x512 over 8 ranks)"
+                                       if args.c3_rank else "")
                                     + f", {args.ksize}^3 PSF, RL {args.psftype} lambda={args.lam}"),
                        "views": args.views, "volume_xyz": [nx, ny_g, nz_g], "psf": [args.ksize] * 3,
                        "fft_dims_xyz": list(M), "local_slabs": args.local_slabs,

@@ -12,8 +12,9 @@ declare -A CFG=(
   [c3x8]="--strong --local-slabs 8 --steps 4 --warmup 1 --no-default-mode --no-strong-line"
   [c4]="--shape 768 768 768 --views 8 --psftype OPTIMIZATION_I --lam 0.006 --steps 4 --warmup 1 --no-default-mode --no-strong-line"
   [c5]="--c5-rank --steps 4 --warmup 1"
+  [c3rank]="--c3-rank --steps 6 --warmup 2"
 )
-for n in headline c3 c3x8 c4 c5; do
+for n in ${CLASSES:-headline c3 c3x8 c3rank c4 c5}; do
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-legacy-line ${CFG[$n]} > $OUT/$n.log 2>&1 || { echo "$n failed"; tail -5 $OUT/$n.log; exit 1; }
   tail -1 $OUT/$n.log > $OUT/$n.json
   python3 - $OUT/$n.json $n <<'PY'
@@ -30,7 +31,9 @@ done
 python3 - $OUT <<'PY'
 import json, os, sys
 out = {}
-for n in ("headline", "c3", "c3x8", "c4", "c5"):
+for n in ("headline", "c3", "c3x8", "c3rank", "c4", "c5"):
+    if not os.path.exists(os.path.join(sys.argv[1], n + ".json")):
+        continue
     d = json.load(open(os.path.join(sys.argv[1], n + ".json")))
     out[n] = {k: d.get(k) for k in ("value", "ms_per_step", "pointwise", "kernel_ms", "roofline", "config", "default_mode")}
 json.dump(out, open(os.path.join(sys.argv[1], "engine_classes.json"), "w"), indent=1)
