@@ -444,8 +444,7 @@ __device__ __forceinline__ DzBox xcd_box(bool xcd) {
 template <int KW, int TY, bool BUF = true, int JT = 0>
 __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restrict__ in, const float2* __restrict__ kx,
                                                 const float2* __restrict__ ky, float2* __restrict__ g12,
-                                                const float* __restrict__ mm, int xcd, int mm_exact, int pz0,
-                                                int npl) {
+                                                const float* __restrict__ mm, int xcd, int mm_exact) {
     constexpr int R = KW / 2;
     constexpr int IW = kDxyTX + KW - 1;          // staged input columns
     constexpr int IP = dxy_in_pitch(IW);         // pitch (see dxy_in_pitch)
@@ -459,7 +458,7 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
     __shared__ __attribute__((aligned(16))) float2 sx[IH * kDxySxP];
     const int nx = int(d.nx), ny = int(d.ny);
     const int gx = (nx + kDxyTX - 1) / kDxyTX, gy = (ny + TY - 1) / TY;
-    const int nstrips = gx * npl;   // planes [pz0, pz0 + npl) (the pipelined DoG launches parts)
+    const int nstrips = gx * int(d.nz);
     const int t = threadIdx.x;
     // FusionHelper.normalizeImage constants (skipped for a NaN / inf / zero range)
     bool norm = false;
@@ -508,7 +507,7 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
         constexpr int NR = decltype(nrc)::value;
         constexpr int NEc = (NR + RPT - 1) / RPT;
         const int x0 = (s % gx) * kDxyTX;
-        const uint32_t plane = uint32_t(pz0 + s / gx) * uint32_t(ny) * uint32_t(nx);
+        const uint32_t plane = uint32_t(s / gx) * uint32_t(ny) * uint32_t(nx);
         const bool inside = x0 - R >= 0 && x0 - R + IW <= nx && ys >= 0 && ys + NR <= ny;
         if (inside) {
             const uint32_t base = plane + uint32_t(ys) * uint32_t(nx) + uint32_t(x0 - R + min(col, IW - 1));
@@ -620,7 +619,7 @@ __global__ __launch_bounds__(256, 4) void k_dog_xy(Dims3 d, const float* __restr
     const int c = t & (kDxyTX - 1), run = t / kDxyTX;
     while (strip < nstrips) {
         const int x0 = (strip % gx) * kDxyTX;
-        const uint32_t plane = uint32_t(pz0 + strip / gx) * uint32_t(ny) * uint32_t(nx);
+        const uint32_t plane = uint32_t(strip / gx) * uint32_t(ny) * uint32_t(nx);
         const int y0 = step * TY;
         const bool pre = step < 0;
         if (pre) norm_store(PREc{}, v);
@@ -1020,7 +1019,7 @@ __global__ __launch_bounds__(BX * BY) void k_dog_z(Dims3 d, const float2* __rest
 template <int KW, int PD, bool ONE, bool ONEG>
 __global__ __launch_bounds__(256) void k_dog_zconv(Dims3 d, const float2* __restrict__ g12,
                                                    const float2* __restrict__ kz, float scale, int zc_len,
-                                                   float* __restrict__ dog, int cbase) {
+                                                   float* __restrict__ dog) {
     constexpr int R = KW / 2;
     constexpr int NW = KW + PD;
     const int nx = int(d.nx), ny = int(d.ny), nz = int(d.nz);
@@ -1031,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_dog_zconv(Dims3 d, const float2* __rest
     if (y >= ny) return;   // (wave-uniform; no barriers in this kernel)
     const int x = (wid % gxw) * 64 + lane;
     const bool valid = x < nx;
-    const int z0 = (cbase + int(blockIdx.y)) * zc_len, z1 = min(nz, z0 + zc_len);
+    const int z0 = int(blockIdx.y) * zc_len, z1 = min(nz, z0 + zc_len);
     const int len = z1 - z0 + KW - 1;   // source planes
     const uint32_t pstride = uint32_t(nx) * uint32_t(ny);
     const uint32_t col = uint32_t(y) * uint32_t(nx) + uint32_t(valid ? x : nx - 1);
@@ -1660,32 +1659,11 @@ struct DogWork {
         if (!stream) SD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         return stream;
     }
-    // the pipelined z stage's stream and its events (created on demand, kept)
-    hipStream_t stream2 = nullptr;
-    std::vector<hipEvent_t> events;
-    hipStream_t get_stream2() {
-        if (!stream2) SD_HIP(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
-        return stream2;
-    }
-    hipEvent_t event(int i) {
-        while (int(events.size()) <= i) {
-            hipEvent_t e;
-            SD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            events.push_back(e);
-        }
-        return events[size_t(i)];
-    }
     void release() {
         if (stream) {
             (void)hipStreamDestroy(stream);
             stream = nullptr;
         }
-        if (stream2) {
-            (void)hipStreamDestroy(stream2);
-            stream2 = nullptr;
-        }
-        for (auto e : events) (void)hipEventDestroy(e);
-        events.clear();
         for (DBuf<float>* b : {&in, &dog, &taps, &mm, &tmp_a, &tmp_b, &tmp_c, &tmp_d}) b->release();
         g12.release();
         keys.release(); keys_sorted.release(); vals.release(); vals_sorted.release();
@@ -1832,8 +1810,10 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
     constexpr int ty = 32;     // strip steps (48-row tiles: 32 measured slower; strips: 32 beat 48, r05_dog_strips_ab.txt)
     constexpr int xcd = 1;     // XCD-contiguous y-fastest boxes of k_dog_z
     constexpr int xcd_xy = 1;  // XCD-contiguous tile ranges of k_dog_xy
-    // k_dog_xy: persistent blocks (up to 4 per CU at 32-row steps: 34.5 KB of LDS each, the
-    // strips spread evenly over them), strips x fastest (launch_xy below)
+    // k_dog_xy: persistent blocks (4 per CU at 32-row steps: 34.5 KB of LDS each), strips x
+    // fastest
+    const int64_t xy_strips = ceil_div(d.nx, kDxyTX) * d.nz;
+    const dim3 gxy(unsigned(std::min<int64_t>(xy_strips, int64_t(256) * 4)));
     // k_dog_z box: 64 x 8 (512 threads); 64 x 16 and 32 x 16 measured slower (r3i)
     constexpr int bx = 64, bz_y = 8;
     // scalar plane indices (one mirror reflection: nz > K / 2; plane bytes in 31 bits)
@@ -1859,62 +1839,24 @@ void dog_run(const float* img, const int64_t* dims, const spim_dog_params* p, fl
         // (k_minmax's own range: the per-value range check is skipped; SPIMDECON_DOG_MM_EXACT=0
         // keeps it -- 1.52-1.62 vs 1.66 ms per 768^3, bit-exact, gpu_r3z11.sh)
         const int mmx = !use_given && dog_env("SPIMDECON_DOG_MM_EXACT", 1) != 0 ? 1 : 0;
-        // Pipelined split z stage (SPIMDECON_DOG_PIPE, default on): k_dog_xy runs over z parts of
-        // H planes on the call's stream, k_dog_zconv over the same chunks on a second stream,
-        // chunk k after the part holding its last source plane (k H + H - 1 + R): the
-        // VALU-bound x / y pass of part k + 2 shares the GPU with the HBM-bound z pass of chunk
-        // k (k_dog_zconv holds no LDS, so its blocks fit beside the persistent x / y blocks).
-        // The same kernels over the same planes: bit-identical to one launch of each.
-        const int H = std::max(1, dog_env("SPIMDECON_DOG_PIPE_CHUNK", 192));
-        const bool pipe = split && dog_env("SPIMDECON_DOG_PIPE", 1) != 0 && d.nz >= 2 * int64_t(H);
-        const int zlen = pipe ? H : zc1;
-        const int nparts = pipe ? int(ceil_div(d.nz, int64_t(H))) : 1;
-        auto launch_xy = [&](int pz0, int npl) {
-            const int64_t strips = ceil_div(d.nx, kDxyTX) * int64_t(npl);
-            const int64_t per = ceil_div(strips, int64_t(256) * 4);   // strips per persistent block
-            const dim3 g(unsigned(ceil_div(strips, per)));
 #define SD_DOGXY3(KV, JV)                                                                                   \
-            if (xbuf) hipLaunchKernelGGL((k_dog_xy<KV, ty, true, JV>), g, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx, pz0, npl); \
-            else hipLaunchKernelGGL((k_dog_xy<KV, ty, false, JV>), g, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx, pz0, npl);
+        if (xbuf) hipLaunchKernelGGL((k_dog_xy<KV, ty, true, JV>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx); \
+        else hipLaunchKernelGGL((k_dog_xy<KV, ty, false, JV>), gxy, dim3(256), 0, s, d, in, kp2(0), kp2(1), w.g12.p, w.mm.p, xcd_xy, mmx);
 #define SD_DOGXY(KV) if (jt == 1) { SD_DOGXY3(KV, 1) } else { SD_DOGXY3(KV, 0) }
-            if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
+        if (K == 7) { SD_DOGXY(7) } else if (K == 15) { SD_DOGXY(15) } else { SD_DOGXY(31) }
 #undef SD_DOGXY
 #undef SD_DOGXY3
-            SD_HIP(hipGetLastError());
-        };
-        auto launch_zc = [&](hipStream_t zs, int cbase, int nch) {
+        SD_HIP(hipGetLastError());
+        if (split) {
             const int64_t waves = ceil_div(d.nx, int64_t(64)) * d.ny;
-            const dim3 gc(unsigned(ceil_div(waves, int64_t(4))), unsigned(nch));
+            const dim3 gc(unsigned(ceil_div(waves, int64_t(4))), unsigned(ceil_div(d.nz, int64_t(zc1))));
             const bool one1 = uint64_t(n) * 4u < 0x80000000ull, oneg = uint64_t(n) * 8u < 0xffffffffull;
-#define SD_DOGZC(KV) if (one1 && oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, true, true>), gc, dim3(256), 0, zs, d, w.g12.p, kp2(2), kinv, zlen, dogp, cbase); \
-            else if (oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, true>), gc, dim3(256), 0, zs, d, w.g12.p, kp2(2), kinv, zlen, dogp, cbase); \
-            else hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, false>), gc, dim3(256), 0, zs, d, w.g12.p, kp2(2), kinv, zlen, dogp, cbase);
+#define SD_DOGZC(KV) if (one1 && oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, true, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else if (oneg) hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, true>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp); \
+            else hipLaunchKernelGGL((k_dog_zconv<KV, kDzcPD, false, false>), gc, dim3(256), 0, s, d, w.g12.p, kp2(2), kinv, zc1, dogp);
             if (K == 7) { SD_DOGZC(7) } else if (K == 15) { SD_DOGZC(15) } else { SD_DOGZC(31) }
 #undef SD_DOGZC
             SD_HIP(hipGetLastError());
-        };
-        if (!pipe) {
-            launch_xy(0, int(d.nz));
-            if (split) launch_zc(s, 0, int(ceil_div(d.nz, int64_t(zlen))));
-        } else {
-            hipStream_t s2 = w.get_stream2();
-            for (int p = 0; p < nparts; ++p) {
-                const int pz0 = p * H;
-                launch_xy(pz0, int(std::min<int64_t>(H, d.nz - pz0)));
-                SD_HIP(hipEventRecord(w.event(p), s));
-            }
-            int waited = -1;
-            for (int k = 0; k < nparts; ++k) {
-                const int64_t last = std::min<int64_t>(d.nz - 1, int64_t(k) * H + H - 1 + K / 2);
-                const int need = int(last / H);
-                if (need > waited) {
-                    SD_HIP(hipStreamWaitEvent(s2, w.event(need), 0));
-                    waited = need;
-                }
-                launch_zc(s2, k, 1);
-            }
-            SD_HIP(hipEventRecord(w.event(nparts), s2));
-            SD_HIP(hipStreamWaitEvent(s, w.event(nparts), 0));
         }
     } else {
         // Gaussians of 63 / 127 taps: the separate passes, then a candidate pass over the DoG

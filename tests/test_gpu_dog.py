@@ -288,23 +288,3 @@ def test_dog_zero_tap_trim_bit_identical(gpu, sigma, monkeypatch):
             out[t] = ([(tuple(p.location), p.intensity) for p in pk], d)
         np.testing.assert_array_equal(out["1"][1], out["0"][1])
         assert out["1"][0] == out["0"][0]
-
-
-@pytest.mark.parametrize("chunk", [64, 96])
-def test_dog_pipelined_z_stage_bit_identical(gpu, chunk, monkeypatch):
-    """The pipelined split z stage (SPIMDECON_DOG_PIPE=1, the default: k_dog_xy over z parts
-    on the call's stream, k_dog_zconv over the same chunks on a second stream once the part
-    holding a chunk's last source plane is done) equals one launch of each (=0), bit for
-    bit, also with a ragged last part (nz 200 at 64- and 96-plane parts)."""
-    img = bead_stack(shape=(200, 44, 72), cid=28)
-    monkeypatch.setenv("SPIMDECON_DOG_PIPE_CHUNK", str(chunk))
-    out = {}
-    for pp in ("1", "0"):
-        monkeypatch.setenv("SPIMDECON_DOG_PIPE", pp)
-        pk, d = dog.compute(img, sigma=1.8, threshold=1e-3, find_min=True, find_max=True, return_dog=True,
-                            keep_intensity=True)
-        out[pp] = ([(tuple(p.location), p.intensity) for p in pk], d)
-    np.testing.assert_array_equal(out["1"][1], out["0"][1])
-    assert out["1"][0] == out["0"][0] and len(out["1"][0]) > 10
-    exp, dref = dog_ref.process_dog(img, 1.8, 1e-3, find_min=True, find_max=True)
-    np.testing.assert_array_equal(out["1"][1], dref)
